@@ -1,0 +1,173 @@
+// api.cpp — the extern "C" boundary declared in include/fa_hip.h.
+//
+// Validates arguments the way the reference's Julia methods would fail
+// (DimensionMismatch → FA_ERR_INVALID_ARG), resolves the default scale
+// τ = 1/√d (src/dense.jl:43), and dispatches to the kernel launchers.  No
+// global state besides the thread-local error string; never allocates,
+// synchronises or aborts.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <string>
+
+#include "../../include/fa_hip.h"
+#include "fa_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fn, const char* msg) {
+    g_last_error = std::string(fn) + ": " + msg;
+    return code;
+}
+
+int ok() {
+    g_last_error.clear();
+    return FA_OK;
+}
+
+bool valid_dtype(int dt) { return dt == FA_DTYPE_F32 || dt == FA_DTYPE_BF16 || dt == FA_DTYPE_F16; }
+
+float resolve_scale(float scale, int64_t d) {
+    if (!(scale > 0.0f) || !std::isfinite(scale)) return (float)(1.0 / std::sqrt((double)d));
+    return scale;
+}
+
+// Window geometry of NNlib.unfold(x, (ws…, d, 1); stride, pad) (src/utils.jl:40).
+int make_geom(fa::WindowGeom& g, int nspatial, const int64_t* spatial, int64_t ws, int64_t stride,
+              int64_t pad, const char** why) {
+    if (nspatial < 1 || nspatial > 3 || !spatial) { *why = "nspatial must be 1, 2 or 3"; return FA_ERR_INVALID_ARG; }
+    if (ws < 1) { *why = "window size must be >= 1"; return FA_ERR_INVALID_ARG; }
+    if (stride < 1) { *why = "stride must be >= 1"; return FA_ERR_INVALID_ARG; }
+    if (pad < 0) pad = (ws - 1) / 2;
+    g.nsp = nspatial;
+    g.ws = ws;
+    g.stride = stride;
+    g.pad = pad;
+    g.T = 1;
+    g.L = 1;
+    g.P = 1;
+    for (int i = 0; i < 3; ++i) { g.S[i] = 1; g.O[i] = 1; }
+    for (int i = 0; i < nspatial; ++i) {
+        if (spatial[i] < 1) { *why = "spatial extents must be >= 1"; return FA_ERR_INVALID_ARG; }
+        const int64_t span = spatial[i] + 2 * pad - ws;
+        if (span < 0) { *why = "window larger than the padded input"; return FA_ERR_INVALID_ARG; }
+        g.S[i] = spatial[i];
+        g.O[i] = span / stride + 1;
+        g.T *= ws;
+        g.L *= g.O[i];
+        g.P *= spatial[i];
+    }
+    return FA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fa_last_error(void) { return g_last_error.c_str(); }
+
+int fa_abi_version(void) { return FA_HIP_ABI_VERSION; }
+
+int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
+
+int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
+                 int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch, float scale,
+                 void* hip_stream) {
+    static const char* fn = "fa_dense_fwd";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, d, dv, batch must be >= 1");
+    if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    fa::DenseArgs a{dtype, Q, K, V, O, l, m, N, Nk, d, dv, batch, resolve_scale(scale, d)};
+    const char* why = "";
+    const int rc = fa::launch_dense_fwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
+size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    if (!valid_dtype(dtype) || N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1) return 0;
+    return fa::dense_bwd_workspace(dtype, N, Nk, d, dv, batch);
+}
+
+int fa_dense_bwd(int dtype, const void* Q, const void* K, const void* V, const void* O, const void* dO,
+                 const float* l, const float* m, void* dQ, void* dK, void* dV, int64_t N, int64_t Nk,
+                 int64_t d, int64_t dv, int64_t batch, float scale, void* workspace,
+                 size_t workspace_bytes, void* hip_stream) {
+    static const char* fn = "fa_dense_bwd";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, d, dv, batch must be >= 1");
+    if (!Q || !K || !V || !O || !dO || !l || !m || !dQ || !dK || !dV)
+        return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    const size_t need = fa::dense_bwd_workspace(dtype, N, Nk, d, dv, batch);
+    if (need > 0 && (!workspace || workspace_bytes < need))
+        return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_dense_bwd_workspace()");
+    fa::DenseBwdArgs a{dtype, Q, K, V, O, dO, l, m, dQ, dK, dV, N, Nk, d, dv, batch,
+                       resolve_scale(scale, d), workspace, workspace_bytes};
+    const char* why = "";
+    const int rc = fa::launch_dense_bwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
+size_t fa_windowed_workspace(int dtype, int nspatial, const int64_t* spatial, int64_t d, int64_t dv,
+                             int64_t batch, int64_t ws, int64_t stride, int64_t pad) {
+    fa::WindowGeom g;
+    const char* why = "";
+    if (!valid_dtype(dtype) || d < 1 || dv < 1 || batch < 1) return 0;
+    if (make_geom(g, nspatial, spatial, ws, stride, pad, &why) != FA_OK) return 0;
+    return fa::windowed_workspace(dtype, g, d, dv, batch);
+}
+
+int fa_windowed_fwd(int dtype, const void* q, const void* k, const void* v, void* y, float* l, float* m,
+                    int nspatial, const int64_t* spatial, int64_t d, int64_t dv, int64_t batch,
+                    int64_t ws, int64_t stride, int64_t pad, float scale, void* hip_stream) {
+    static const char* fn = "fa_windowed_fwd";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (d < 1 || dv < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv, batch must be >= 1");
+    if (!q || !k || !v || !y || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    fa::WindowedArgs a{};
+    const char* why = "";
+    int rc = make_geom(a.g, nspatial, spatial, ws, stride, pad, &why);
+    if (rc != FA_OK) return fail(rc, fn, why);
+    a.dtype = dtype; a.q = q; a.k = k; a.v = v; a.y = y; a.l = l; a.m = m;
+    a.d = d; a.dv = dv; a.batch = batch;
+    a.scale = resolve_scale(scale, d);
+    a.workspace = nullptr;
+    a.workspace_bytes = 0;
+    rc = fa::launch_windowed_fwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
+int fa_windowed_bwd(int dtype, const void* q, const void* k, const void* v, const void* y, const void* dy,
+                    const float* l, const float* m, void* dq, void* dk, void* dv_, int nspatial,
+                    const int64_t* spatial, int64_t d, int64_t dv, int64_t batch, int64_t ws,
+                    int64_t stride, int64_t pad, float scale, void* workspace, size_t workspace_bytes,
+                    void* hip_stream) {
+    static const char* fn = "fa_windowed_bwd";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (d < 1 || dv < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv, batch must be >= 1");
+    if (!q || !k || !v || !y || !dy || !l || !m || !dq || !dk || !dv_)
+        return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    fa::WindowedBwdArgs a{};
+    const char* why = "";
+    int rc = make_geom(a.g, nspatial, spatial, ws, stride, pad, &why);
+    if (rc != FA_OK) return fail(rc, fn, why);
+    const size_t need = fa::windowed_workspace(dtype, a.g, d, dv, batch);
+    if (need > 0 && (!workspace || workspace_bytes < need))
+        return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_windowed_workspace()");
+    a.dtype = dtype; a.q = q; a.k = k; a.v = v; a.y = y; a.dy = dy; a.l = l; a.m = m;
+    a.dq = dq; a.dk = dk; a.dv_ = dv_;
+    a.d = d; a.dv = dv; a.batch = batch;
+    a.scale = resolve_scale(scale, d);
+    a.workspace = workspace;
+    a.workspace_bytes = workspace_bytes;
+    rc = fa::launch_windowed_bwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
+}  // extern "C"

@@ -1,0 +1,516 @@
+// fa_fwd.hip — dense flash-attention forward for gfx950 (MI355X, CDNA4).
+//
+// Replaces the blockwise forward dense_fa!(O, l, m, Q, K, V)
+// (reference src/dense.jl:21-102).  Same result — O = softmax(τ Q Kᵀ) V with
+// l = Σ exp(s − m), m = max s per query row (src/dense.jl:78-91) — computed
+// MI355X-first rather than translated:
+//
+//  * one workgroup = 4 waves = 128 query rows of one batch slab; each wave owns
+//    32 query rows for the whole key sweep (FA-2 order: O accumulates
+//    unnormalised in fp32 registers and is divided by l once at the end; the
+//    reference renormalises O every tile, src/dense.jl:89 — mathematically
+//    equal, documented in DESIGN.md);
+//  * key/value tiles of 64 tokens are staged HBM → registers → LDS (issue the
+//    next tile's global loads before computing the current one, write them
+//    after the tile's barrier: async-STAGE split);
+//  * both tile products run on MFMA.  Scores are computed TRANSPOSED,
+//    Sᵀ = K·Qᵀ (keys on accumulator rows / registers, queries on lanes), so the
+//    fp32 score tile converted to bf16 is already the B operand of Oᵀ = Vᵀ·Pᵀ:
+//    no LDS round trip for P, and row max / row sum are register reductions
+//    plus one v_permlane32_swap;
+//  * the reference layout keeps tokens contiguous, so the QKᵀ contraction
+//    (over features) is strided: K tiles are read with the gfx950 transpose
+//    read ds_read_b64_tr_b16 from an XOR-swizzled image (conflict-free), while
+//    Vᵀ fragments (contraction over tokens, contiguous) are plain ds_read_b128
+//    from a padded image (conflict-free);
+//  * the key order inside each 16-key group of a K fragment is permuted
+//    (bits 2 and 3 swapped) so that each lane's 8 bf16 P values cover 8
+//    CONSECUTIVE keys, which makes the Vᵀ fragment one 16-byte read;
+//  * exp2 with τ·log2(e) folded into one FMA; the running max is kept in raw
+//    dot-product units and converted to natural-log units (m = τ·max) on store;
+//  * ragged N / Nk: keys past Nk get score −inf (the reference CUDA kernel
+//    zero-fills them, src/cuda/flash.jl:45 — Appendix A.4, not inherited),
+//    queries past N are computed on zeros and not stored;
+//  * head dims are padded (zero features) to the compiled class 32/64/128,
+//    so the reference's own test shape (dqk = 12, dv = 6, test/test.jl:6-10)
+//    runs on the same kernels;
+//  * blockIdx is remapped so that all workgroups of one batch slab share an
+//    XCD (its 4 MiB L2 then serves the slab's K/V re-reads).
+//
+// fp32 inputs use the exact-f32 MFMA v_mfma_f32_32x32x2_f32 (no TF32 on
+// gfx950) with the same structure; that path exists for fp32 parity, the
+// performance path is bf16 / fp16.
+#include "fa_common.h"
+#include "fa_internal.h"
+#include "../../include/fa_hip.h"
+
+namespace fa {
+
+struct FwdParams {
+    const void* Q;
+    const void* K;
+    const void* V;
+    void* O;
+    float* l;
+    float* m;
+    int N, Nk, d, dv;
+    int nqb, total_wg;
+    float scale, scale_log2;
+    int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
+};
+
+constexpr int kBM = 128;  // query rows per workgroup (4 waves x 32)
+constexpr int kBN = 64;   // keys per tile
+constexpr int kThreads = 256;
+
+// One 16-byte chunk (16/sizeof(T) elements) of row `row`, columns
+// [col0, col0+EPC) of a row-major [nrows][ncols] slab; zero out of range.
+template <class T>
+__device__ __forceinline__ u32x4 load_chunk(const T* base, int row, int col0, int nrows,
+                                            int ncols, bool fast) {
+    constexpr int EPC = 16 / sizeof(T);
+    u32x4 z = {0u, 0u, 0u, 0u};
+    if (row >= nrows) return z;
+    const T* src = base + (int64_t)row * ncols;
+    if (fast) {
+        if (col0 >= ncols) return z;
+        return *(const u32x4*)(src + col0);
+    }
+    union {
+        T e[EPC];
+        u32x4 v;
+    } u;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) u.e[e] = (col0 + e < ncols) ? src[col0 + e] : (T)0.0f;
+    return u.v;
+}
+
+// --------------------------------------------------------------------------
+// bf16 / fp16 forward (v_mfma_f32_32x32x16_{bf16,f16})
+// --------------------------------------------------------------------------
+template <class T, int D, int DV>
+__global__ __launch_bounds__(kThreads) void dense_fwd_mfma16(FwdParams p) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int KROW = kBN * 2;       // K image: [D][64 keys], 128-B rows, 32-B chunk XOR swizzle
+    constexpr int VROW = kBN * 2 + 16;  // V image: [DV][64 keys], 144-B rows (pad → conflict-free b128)
+    constexpr int KCH = D * 8 / kThreads;   // 16-B K chunks per thread per tile
+    constexpr int VCH = DV * 8 / kThreads;
+    static_assert(KCH >= 1 && VCH >= 1, "head dim class too small");
+    __shared__ __attribute__((aligned(16))) char smem[D * KROW + DV * VROW];
+    char* const klds = smem;
+    char* const vlds = smem + D * KROW;
+
+    const int lid = xcd_remap(blockIdx.x, p.total_wg);
+    const int b = lid / p.nqb;
+    const int qb = lid - b * p.nqb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
+    const T* __restrict__ Qb = (const T*)p.Q + (int64_t)b * N * d;
+    const T* __restrict__ Kb = (const T*)p.K + (int64_t)b * Nk * d;
+    const T* __restrict__ Vb = (const T*)p.V + (int64_t)b * Nk * dv;
+    const bool fast = p.fast != 0;
+
+    // Q^T fragments (B operand of S^T = K Q^T), kept in registers:
+    // lane (r, h), k-step s holds Q[query qi][features 16s+8h .. 16s+8h+7].
+    const int qi = qb * kBM + wave * 32 + r;
+    F8 qf[D / 16];
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int f = 16 * s + 8 * h + e;
+            qf[s][e] = (qi < N && f < d) ? Qb[(int64_t)f * N + qi] : (T)0.0f;
+        }
+
+    // Per-lane LDS offsets of the transposed K reads.  16-lane group g: kh = g&1
+    // selects keys 0-15 / 16-31 of a 32-key block; lane 4q+pp supplies feature
+    // row q and the 4-key chunk sigma(pp) (sigma swaps 1 and 2 → lane r ends up
+    // holding key pi(r) = r with bits 2 and 3 swapped).
+    const int g = lane >> 4, kh = g & 1, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    int koff[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+        koff[kb] = (8 * h + qq) * KROW + (((kb * 2 + kh) ^ (((qq >> 1) & 1) << 1)) * 32) + 8 * sig;
+    const int voff = r * VROW + 16 * h;  // + cb*32*VROW + (kb*32+16s)*2
+
+    f32x16 oacc[DV / 32];
+#pragma unroll
+    for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) oacc[cb][x] = 0.0f;
+    float m_run = kNegInf, l_run = 0.0f;
+    const float c = p.scale_log2;
+
+    u32x4 kreg[KCH], vreg[VCH];
+    auto gload = [&](int j) {
+        const int key0 = j * kBN;
+#pragma unroll
+        for (int it = 0; it < KCH; ++it) {
+            const int ch = tid + kThreads * it;
+            kreg[it] = load_chunk<T>(Kb, ch >> 3, key0 + (ch & 7) * 8, d, Nk, fast);
+        }
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) {
+            const int ch = tid + kThreads * it;
+            vreg[it] = load_chunk<T>(Vb, ch >> 3, key0 + (ch & 7) * 8, dv, Nk, fast);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int it = 0; it < KCH; ++it) {
+            const int ch = tid + kThreads * it, f = ch >> 3, pc = ch & 7;
+            const int off = f * KROW + (((pc >> 1) ^ (((f >> 1) & 1) << 1)) * 32) + (pc & 1) * 16;
+            *(u32x4*)(klds + off) = kreg[it];
+        }
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) {
+            const int ch = tid + kThreads * it;
+            *(u32x4*)(vlds + (ch >> 3) * VROW + (ch & 7) * 16) = vreg[it];
+        }
+    };
+
+    const int ntiles = (Nk + kBN - 1) / kBN;
+    gload(0);
+    lstore();
+    __syncthreads();
+
+    for (int j = 0; j < ntiles; ++j) {
+        const bool more = j + 1 < ntiles;
+        if (more) gload(j + 1);
+
+        // ---- S^T = K Q^T : two 32-key accumulator blocks ----
+        f32x16 sacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sacc[kb][x] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) {
+                const char* a = klds + koff[kb] + 16 * s * KROW;
+                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW));
+                const F8 af = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                sacc[kb] = mfma32x32x16(af, qf[s], sacc[kb]);
+            }
+        }
+
+        // ---- mask keys >= Nk (last tile only) ----
+        const int key0 = j * kBN;
+        if (key0 + kBN > Nk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) {
+                    const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+                    if (key0 + kt >= Nk) sacc[kb][x] = kNegInf;
+                }
+        }
+
+        // ---- online softmax (raw dot-product units; exp2 with folded scale) ----
+        float mt = kNegInf;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) mt = fmaxf(mt, sacc[kb][x]);
+        mt = swap_halves_max(mt);
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = exp2_fast((m_run - m_new) * c);
+        const float mc = m_new * c;
+        float ls = 0.0f;
+        F8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pv = exp2_fast(fmaf(sacc[kb][x], c, -mc));
+                ls += pv;
+                pf[kb][x >> 3][x & 7] = (T)pv;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oacc[cb][x] *= alpha;
+
+        // ---- O^T += V^T P^T ----
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const F8 va = *(const F8*)(vlds + voff + cb * 32 * VROW + (kb * 32 + 16 * s) * 2);
+                    oacc[cb] = mfma32x32x16(va, pf[kb][s], oacc[cb]);
+                }
+
+        __syncthreads();
+        if (more) {
+            lstore();
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: O = O / l ; l, m in natural-log units ----
+    const float lt = swap_halves_sum(l_run);
+    const float inv = 1.0f / lt;
+    if (qi < N) {
+        T* Ob = (T*)p.O + (int64_t)b * N * dv;
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = cb * 32 + acc_row(x, h);
+                if (cc < dv) Ob[(int64_t)cc * N + qi] = (T)(oacc[cb][x] * inv);
+            }
+        if (h == 0) {
+            p.m[(int64_t)b * N + qi] = m_run * p.scale;
+            p.l[(int64_t)b * N + qi] = lt;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// fp32 forward (exact f32 MFMA v_mfma_f32_32x32x2_f32)
+// --------------------------------------------------------------------------
+template <int D, int DV>
+__global__ __launch_bounds__(kThreads) void dense_fwd_f32(FwdParams p) {
+    constexpr int KROWF = kBN;       // K image [D][64] floats
+    constexpr int VROWF = kBN + 1;   // V image [DV][65] floats (pad → conflict-free column reads)
+    constexpr int KCH = D * 16 / kThreads;
+    constexpr int VCH = DV * 16 / kThreads;
+    static_assert(KCH >= 1 && VCH >= 1, "head dim class too small");
+    __shared__ __attribute__((aligned(16))) float smem[D * KROWF + DV * VROWF];
+    float* const klds = smem;
+    float* const vlds = smem + D * KROWF;
+
+    const int lid = xcd_remap(blockIdx.x, p.total_wg);
+    const int b = lid / p.nqb;
+    const int qb = lid - b * p.nqb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
+    const float* __restrict__ Qb = (const float*)p.Q + (int64_t)b * N * d;
+    const float* __restrict__ Kb = (const float*)p.K + (int64_t)b * Nk * d;
+    const float* __restrict__ Vb = (const float*)p.V + (int64_t)b * Nk * dv;
+    const bool fast = p.fast != 0;
+
+    const int qi = qb * kBM + wave * 32 + r;
+    float qf[D / 2];  // lane (r, h), step t: Q[qi][feature 2t+h]
+#pragma unroll
+    for (int t = 0; t < D / 2; ++t) {
+        const int f = 2 * t + h;
+        qf[t] = (qi < N && f < d) ? Qb[(int64_t)f * N + qi] : 0.0f;
+    }
+
+    f32x16 oacc[DV / 32];
+#pragma unroll
+    for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) oacc[cb][x] = 0.0f;
+    float m_run = kNegInf, l_run = 0.0f;
+    const float c = p.scale_log2;
+
+    u32x4 kreg[KCH], vreg[VCH];
+    auto gload = [&](int j) {
+        const int key0 = j * kBN;
+#pragma unroll
+        for (int it = 0; it < KCH; ++it) {
+            const int ch = tid + kThreads * it;
+            kreg[it] = load_chunk<float>(Kb, ch >> 4, key0 + (ch & 15) * 4, d, Nk, fast);
+        }
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) {
+            const int ch = tid + kThreads * it;
+            vreg[it] = load_chunk<float>(Vb, ch >> 4, key0 + (ch & 15) * 4, dv, Nk, fast);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int it = 0; it < KCH; ++it) {
+            const int ch = tid + kThreads * it;
+            *(u32x4*)(klds + (ch >> 4) * KROWF + (ch & 15) * 4) = kreg[it];
+        }
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) {
+            const int ch = tid + kThreads * it;
+            float* dst = vlds + (ch >> 4) * VROWF + (ch & 15) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dst[e] = __uint_as_float(vreg[it][e]);
+        }
+    };
+
+    const int ntiles = (Nk + kBN - 1) / kBN;
+    gload(0);
+    lstore();
+    __syncthreads();
+
+    for (int j = 0; j < ntiles; ++j) {
+        const bool more = j + 1 < ntiles;
+        if (more) gload(j + 1);
+
+        f32x16 sacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sacc[kb][x] = 0.0f;
+#pragma unroll
+            for (int t = 0; t < D / 2; ++t)
+                sacc[kb] = mfma32x32x2(klds[(2 * t + h) * KROWF + kb * 32 + r], qf[t], sacc[kb]);
+        }
+
+        const int key0 = j * kBN;
+        if (key0 + kBN > Nk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x)
+                    if (key0 + kb * 32 + acc_row(x, h) >= Nk) sacc[kb][x] = kNegInf;
+        }
+
+        float mt = kNegInf;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) mt = fmaxf(mt, sacc[kb][x]);
+        mt = swap_halves_max(mt);
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = exp2_fast((m_run - m_new) * c);
+        const float mc = m_new * c;
+        float ls = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pv = exp2_fast(fmaf(sacc[kb][x], c, -mc));
+                ls += pv;
+                sacc[kb][x] = pv;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oacc[cb][x] *= alpha;
+
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x)
+                    oacc[cb] = mfma32x32x2(vlds[(cb * 32 + r) * VROWF + kb * 32 + acc_row(x, h)],
+                                           sacc[kb][x], oacc[cb]);
+
+        __syncthreads();
+        if (more) {
+            lstore();
+            __syncthreads();
+        }
+    }
+
+    const float lt = swap_halves_sum(l_run);
+    const float inv = 1.0f / lt;
+    if (qi < N) {
+        float* Ob = (float*)p.O + (int64_t)b * N * dv;
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = cb * 32 + acc_row(x, h);
+                if (cc < dv) Ob[(int64_t)cc * N + qi] = oacc[cb][x] * inv;
+            }
+        if (h == 0) {
+            p.m[(int64_t)b * N + qi] = m_run * p.scale;
+            p.l[(int64_t)b * N + qi] = lt;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// launcher
+// --------------------------------------------------------------------------
+template <class T, int D>
+static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
+    switch (DVc) {
+        case 32: hipLaunchKernelGGL((dense_fwd_mfma16<T, D, 32>), grid, dim3(kThreads), 0, s, p); break;
+        case 64: hipLaunchKernelGGL((dense_fwd_mfma16<T, D, 64>), grid, dim3(kThreads), 0, s, p); break;
+        case 128: hipLaunchKernelGGL((dense_fwd_mfma16<T, D, 128>), grid, dim3(kThreads), 0, s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+template <int D>
+static hipError_t launch_dv_f32(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
+    switch (DVc) {
+        case 32: hipLaunchKernelGGL((dense_fwd_f32<D, 32>), grid, dim3(kThreads), 0, s, p); break;
+        case 64: hipLaunchKernelGGL((dense_fwd_f32<D, 64>), grid, dim3(kThreads), 0, s, p); break;
+        case 128: hipLaunchKernelGGL((dense_fwd_f32<D, 128>), grid, dim3(kThreads), 0, s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+template <class T>
+static hipError_t launch_typed(const FwdParams& p, int Dc, int DVc, dim3 grid, hipStream_t s) {
+    switch (Dc) {
+        case 32: return launch_dv<T, 32>(p, DVc, grid, s);
+        case 64: return launch_dv<T, 64>(p, DVc, grid, s);
+        case 128: return launch_dv<T, 128>(p, DVc, grid, s);
+    }
+    return hipErrorInvalidValue;
+}
+static hipError_t launch_f32(const FwdParams& p, int Dc, int DVc, dim3 grid, hipStream_t s) {
+    switch (Dc) {
+        case 32: return launch_dv_f32<32>(p, DVc, grid, s);
+        case 64: return launch_dv_f32<64>(p, DVc, grid, s);
+        case 128: return launch_dv_f32<128>(p, DVc, grid, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+
+int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
+    const int Dc = head_dim_class(a.d), DVc = head_dim_class(a.dv);
+    if (!Dc || !DVc) {
+        *why = "head dimension exceeds the compiled maximum (128)";
+        return FA_ERR_UNSUPPORTED;
+    }
+    if (a.N > INT32_MAX / 2 || a.Nk > INT32_MAX / 2 || a.N * a.d > INT32_MAX ||
+        a.Nk * a.d > INT32_MAX || a.Nk * a.dv > INT32_MAX || a.N * a.dv > INT32_MAX) {
+        *why = "per-slab extent exceeds 2^31 elements";
+        return FA_ERR_UNSUPPORTED;
+    }
+    FwdParams p;
+    p.Q = a.Q; p.K = a.K; p.V = a.V; p.O = a.O; p.l = a.l; p.m = a.m;
+    p.N = (int)a.N; p.Nk = (int)a.Nk; p.d = (int)a.d; p.dv = (int)a.dv;
+    p.nqb = (int)((a.N + kBM - 1) / kBM);
+    const int64_t total = (int64_t)p.nqb * a.batch;
+    if (total > INT32_MAX) {
+        *why = "grid too large";
+        return FA_ERR_UNSUPPORTED;
+    }
+    p.total_wg = (int)total;
+    p.scale = a.scale;
+    p.scale_log2 = a.scale * kLog2e;
+    const int epc = a.dtype == FA_DTYPE_F32 ? 4 : 8;
+    p.fast = (a.Nk % epc == 0) && aligned16(a.K) && aligned16(a.V);
+    const dim3 grid((unsigned)total);
+    hipError_t e;
+    switch (a.dtype) {
+        case FA_DTYPE_BF16: e = launch_typed<bf16>(p, Dc, DVc, grid, s); break;
+        case FA_DTYPE_F16: e = launch_typed<f16>(p, Dc, DVc, grid, s); break;
+        case FA_DTYPE_F32: e = launch_f32(p, Dc, DVc, grid, s); break;
+        default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
+    }
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return FA_ERR_HIP;
+    }
+    return FA_OK;
+}
+
+}  // namespace fa

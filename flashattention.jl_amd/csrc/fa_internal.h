@@ -1,0 +1,83 @@
+// fa_internal.h — host-side launcher interface between api.cpp (argument
+// validation, C ABI) and the kernel translation units.  Not installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace fa {
+
+struct DenseArgs {
+    int dtype;                 // fa_dtype
+    const void *Q, *K, *V;
+    void* O;
+    float *l, *m;
+    int64_t N, Nk, d, dv, batch;
+    float scale;               // already resolved (> 0)
+};
+
+struct DenseBwdArgs {
+    int dtype;
+    const void *Q, *K, *V, *O, *dO;
+    const float *l, *m;
+    void *dQ, *dK, *dV;
+    int64_t N, Nk, d, dv, batch;
+    float scale;
+    void* workspace;
+    size_t workspace_bytes;
+};
+
+struct WindowGeom {
+    int nsp;                   // spatial rank 1..3
+    int64_t S[3];              // spatial extents (first = fastest)
+    int64_t O[3];              // windows per dim
+    int64_t ws, stride, pad;
+    int64_t T;                 // ws^nsp tokens per window
+    int64_t L;                 // windows per image
+    int64_t P;                 // pixels per image
+};
+
+struct WindowedArgs {
+    int dtype;
+    const void *q, *k, *v;
+    void* y;
+    float *l, *m;
+    WindowGeom g;
+    int64_t d, dv, batch;
+    float scale;
+    void* workspace;
+    size_t workspace_bytes;
+};
+
+struct WindowedBwdArgs {
+    int dtype;
+    const void *q, *k, *v, *y, *dy;
+    const float *l, *m;
+    void *dq, *dk, *dv_;
+    WindowGeom g;
+    int64_t d, dv, batch;
+    float scale;
+    void* workspace;
+    size_t workspace_bytes;
+};
+
+// Each returns a hipError_t-like code through *err and a fa_status.
+int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
+size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
+int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why);
+size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
+int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why);
+int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why);
+
+// Padded head-dim class a kernel is compiled for: 32, 64 or 128 (0 = none).
+inline int head_dim_class(int64_t d) {
+    if (d <= 32) return 32;
+    if (d <= 64) return 64;
+    if (d <= 128) return 128;
+    return 0;
+}
+
+constexpr int kMaxHeadDim = 128;
+
+}  // namespace fa

@@ -1,0 +1,350 @@
+"""fa_hip — Python host mirror of FlashAttention.jl's attention API over the
+MI355X C ABI (``include/fa_hip.h``, ``libfa_hip.so``).
+
+The reference API is Julia (nikopj/FlashAttention.jl); this module mirrors it
+name for name so the parity tests read like the reference's own tests:
+
+=========================================  ===========================================
+reference (Julia)                          here (torch tensors on a ROCm device)
+=========================================  ===========================================
+``dense_fa(q, k, v) -> (y, l, m)``         :func:`dense_fa`        src/dense.jl:1-19
+``dense_fa!(O, l, m, Q, K, V)``            :func:`dense_fa_`       src/dense.jl:21-102
+``dense_fa_backward(Q,K,V,O,dO,l,m)``      :func:`dense_fa_backward` src/dense.jl:104-167
+``windowed_fa(q,k,v,ws; stride, pad)``     :func:`windowed_fa`     src/windowed.jl:3-23
+``block_fa(q,k,v,ws; pad=0)``              :func:`block_fa`        src/windowed.jl:1
+=========================================  ===========================================
+
+Arrays carry the reference's **Julia shapes and column-major layout**: a Julia
+``(N, d, B)`` array is a torch tensor of shape ``(N, d, B)`` with strides
+``(1, N, N*d)`` (create them with :func:`jl_empty` / :func:`jl_tensor`).  The
+C ABI receives the raw device pointers, so no copy or transpose happens at the
+boundary.  ``l`` and ``m`` are float32 for every input dtype.
+
+Errors mirror the reference: shape problems raise :class:`DimensionMismatch`
+(Julia ``DimensionMismatch``); failures reported by the library raise
+:class:`FlashAttentionError` carrying ``fa_last_error()``.  There is no CPU
+fallback: if ``libfa_hip.so`` is missing, importing the bindings fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+__all__ = [
+    "DimensionMismatch", "FlashAttentionError", "lib", "lib_path",
+    "jl_empty", "jl_zeros", "jl_tensor", "jl_strides", "is_jl_contiguous",
+    "dense_fa", "dense_fa_", "dense_fa_backward", "windowed_fa", "block_fa",
+    "windowed_fa_backward", "window_geometry", "DTYPES",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+
+
+class DimensionMismatch(ValueError):
+    """Raised where the reference's Julia code throws ``DimensionMismatch``."""
+
+
+class FlashAttentionError(RuntimeError):
+    """A nonzero ``fa_status`` from the C ABI; message = ``fa_last_error()``."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"[fa_status {status}] {message}")
+        self.status = status
+
+
+FA_OK, FA_ERR_INVALID_ARG, FA_ERR_UNSUPPORTED, FA_ERR_HIP, FA_ERR_WORKSPACE = range(5)
+DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+# ----------------------------------------------------------------------------
+# library loading (the C ABI is the only compute path)
+# ----------------------------------------------------------------------------
+_LIB = None
+
+
+def lib_path() -> str:
+    return os.environ.get("FA_HIP_LIB", os.path.join(_PKG, "libfa_hip.so"))
+
+
+def lib() -> ctypes.CDLL:
+    """Load ``libfa_hip.so`` (built by ``__graft_entry__.build()``).
+
+    torch is imported first so the library binds torch's already-loaded HIP
+    runtime (same soname), i.e. device pointers and streams are shared.
+    """
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise ImportError(
+            f"fa_hip: native library not found at {path}; run __graft_entry__.build() "
+            "(there is deliberately no CPU fallback)")
+    L = ctypes.CDLL(path)
+    i64, f32, vp = ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+    fp = ctypes.POINTER(ctypes.c_float)
+    L.fa_last_error.restype = ctypes.c_char_p
+    L.fa_abi_version.restype = ctypes.c_int
+    L.fa_max_head_dim.restype = ctypes.c_int
+    L.fa_dense_fwd.restype = ctypes.c_int
+    L.fa_dense_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp]
+    L.fa_dense_bwd_workspace.restype = ctypes.c_size_t
+    L.fa_dense_bwd_workspace.argtypes = [ctypes.c_int, i64, i64, i64, i64, i64]
+    L.fa_dense_bwd.restype = ctypes.c_int
+    L.fa_dense_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                               i64, i64, i64, i64, i64, f32, vp, ctypes.c_size_t, vp]
+    L.fa_windowed_workspace.restype = ctypes.c_size_t
+    L.fa_windowed_workspace.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64),
+                                        i64, i64, i64, i64, i64, i64]
+    L.fa_windowed_fwd.restype = ctypes.c_int
+    L.fa_windowed_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, ctypes.c_int,
+                                  ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64, f32, vp]
+    L.fa_windowed_bwd.restype = ctypes.c_int
+    L.fa_windowed_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                  ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64,
+                                  f32, vp, ctypes.c_size_t, vp]
+    del fp
+    if L.fa_abi_version() != 1:
+        raise ImportError("fa_hip: ABI version mismatch")
+    _LIB = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != FA_OK:
+        msg = lib().fa_last_error().decode(errors="replace")
+        if rc == FA_ERR_INVALID_ARG and "DimensionMismatch" in msg:
+            raise DimensionMismatch(msg)
+        raise FlashAttentionError(rc, msg)
+
+
+# ----------------------------------------------------------------------------
+# Julia-layout tensors
+# ----------------------------------------------------------------------------
+def jl_strides(shape: Sequence[int]) -> Tuple[int, ...]:
+    st, acc = [], 1
+    for s in shape:
+        st.append(acc)
+        acc *= int(s)
+    return tuple(st)
+
+
+def is_jl_contiguous(t: torch.Tensor) -> bool:
+    """True if ``t`` is laid out like a Julia Array of the same shape."""
+    return all(sz == 1 or st == js for sz, st, js in zip(t.shape, t.stride(), jl_strides(t.shape)))
+
+
+def jl_empty(shape: Sequence[int], dtype=torch.float32, device="cuda") -> torch.Tensor:
+    """Uninitialised tensor with Julia shape ``shape`` and column-major strides."""
+    shape = tuple(int(s) for s in shape)
+    n = len(shape)
+    return torch.empty(tuple(reversed(shape)), dtype=dtype, device=device).permute(*reversed(range(n)))
+
+
+def jl_zeros(shape: Sequence[int], dtype=torch.float32, device="cuda") -> torch.Tensor:
+    t = jl_empty(shape, dtype, device)
+    t.zero_()
+    return t
+
+
+def jl_tensor(x, dtype=torch.float32, device="cuda") -> torch.Tensor:
+    """Copy array-like ``x`` (indexed by Julia shape) into a column-major tensor."""
+    src = torch.as_tensor(x)
+    t = jl_empty(src.shape, dtype, device)
+    t.copy_(src)
+    return t
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _require(cond: bool, msg: str) -> None:
+    if not cond:
+        raise DimensionMismatch(msg)
+
+
+def _dtype_code(*ts: torch.Tensor) -> int:
+    dt = ts[0].dtype
+    for t in ts:
+        _require(t.dtype == dt, f"mixed element types {dt} and {t.dtype}")
+    if dt not in DTYPES:
+        raise TypeError(f"unsupported element type {dt}; use float32, bfloat16 or float16")
+    return DTYPES[dt]
+
+
+def _device_check(*ts: torch.Tensor) -> None:
+    dev = ts[0].device
+    if dev.type != "cuda":
+        raise TypeError("fa_hip computes on the ROCm device only (no CPU fallback); "
+                        "move arrays to 'cuda'")
+    for t in ts:
+        _require(t.device == dev, "arrays on different devices")
+        _require(is_jl_contiguous(t), "arrays must be column-major (Julia) contiguous; "
+                 "use fa_hip.jl_tensor / jl_empty")
+
+
+# ----------------------------------------------------------------------------
+# dense
+# ----------------------------------------------------------------------------
+def dense_fa_(O: torch.Tensor, l: torch.Tensor, m: torch.Tensor,
+              Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor,
+              scale: float = 0.0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """``dense_fa!(O, l, m, Q, K, V)`` — src/dense.jl:21-102, in place.
+
+    Q (N, d, B), K (Nk, d, B), V (Nk, dv, B), O (N, dv, B); l, m (N, 1, B)
+    float32.  Returns ``(O, l, m)`` like the reference (:101).
+    """
+    for t in (O, l, m, Q, K, V):
+        _require(t.dim() == 3, "dense_fa! expects 3-D (N, d, batch) arrays")
+    N, d, B = Q.shape
+    Nk, dv = K.shape[0], V.shape[1]
+    _require(K.shape == (Nk, d, B), f"K has shape {tuple(K.shape)}, expected ({Nk}, {d}, {B})")
+    _require(V.shape == (Nk, dv, B), f"V has shape {tuple(V.shape)}, expected ({Nk}, {dv}, {B})")
+    _require(O.shape == (N, dv, B), f"O has shape {tuple(O.shape)}, expected ({N}, {dv}, {B})")
+    _require(l.shape == (N, 1, B) and m.shape == (N, 1, B), "l, m must be (N, 1, batch)")
+    _require(l.dtype == torch.float32 and m.dtype == torch.float32, "l, m must be float32")
+    code = _dtype_code(Q, K, V, O)
+    _device_check(Q, K, V, O, l, m)
+    _check(lib().fa_dense_fwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
+                              N, Nk, d, dv, B, float(scale), _stream(Q)))
+    return O, l, m
+
+
+def dense_fa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float = 0.0):
+    """``dense_fa(q, k, v) -> (y, l, m)`` — src/dense.jl:1-19.
+
+    q, k: (spatial..., d, B); v: (spatial..., dv, B).  Spatial dims are
+    flattened column-major into N (:6-8).  y: (spatial..., dv, B); l, m:
+    (N, 1, B) float32 with l = Σ exp(s − m), m = max s (natural-log units).
+    """
+    _require(q.dim() >= 3 and k.dim() == q.dim() and v.dim() == q.dim(),
+             "q, k, v must share rank >= 3")
+    D = q.dim()
+    d, B = q.shape[D - 2], q.shape[D - 1]
+    dv = v.shape[D - 2]
+    _device_check(q, k, v)
+    N = math.prod(q.shape[: D - 2])
+    Nk = math.prod(k.shape[: D - 2])
+    _require(k.shape[D - 2:] == (d, B), "k must be (spatial..., d, batch)")
+    _require(math.prod(v.shape[: D - 2]) == Nk and v.shape[D - 1] == B,
+             "v must have k's token count and batch")
+    Q = q.as_strided((N, d, B), jl_strides((N, d, B)))
+    K = k.as_strided((Nk, d, B), jl_strides((Nk, d, B)))
+    V = v.as_strided((Nk, dv, B), jl_strides((Nk, dv, B)))
+    O = jl_empty((N, dv, B), q.dtype, q.device)
+    l = jl_empty((N, 1, B), torch.float32, q.device)
+    m = jl_empty((N, 1, B), torch.float32, q.device)
+    dense_fa_(O, l, m, Q, K, V, scale)
+    y = O.as_strided(tuple(q.shape[: D - 2]) + (dv, B), jl_strides(tuple(q.shape[: D - 2]) + (dv, B)))
+    return y, l, m
+
+
+def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
+    """``dense_fa_backward(Q, K, V, O, dO, l, m) -> (dQ, dK, dV)`` —
+    src/dense.jl:104-167 (executable spec src_cpp/FlashAttention.cpp:194-252)."""
+    for t in (Q, K, V, O, dO, l, m):
+        _require(t.dim() == 3, "dense_fa_backward expects 3-D (N, d, batch) arrays")
+    N, d, B = Q.shape
+    Nk, dv = K.shape[0], V.shape[1]
+    _require(K.shape == (Nk, d, B) and V.shape == (Nk, dv, B), "K, V shapes disagree with Q")
+    _require(O.shape == (N, dv, B) and dO.shape == (N, dv, B), "O, dO must be (N, dv, batch)")
+    _require(l.shape == (N, 1, B) and m.shape == (N, 1, B), "l, m must be (N, 1, batch)")
+    code = _dtype_code(Q, K, V, O, dO)
+    _device_check(Q, K, V, O, dO, l, m)
+    dQ = jl_empty((N, d, B), Q.dtype, Q.device)
+    dK = jl_empty((Nk, d, B), Q.dtype, Q.device)
+    dV = jl_empty((Nk, dv, B), Q.dtype, Q.device)
+    L = lib()
+    nws = L.fa_dense_bwd_workspace(code, N, Nk, d, dv, B)
+    ws = torch.empty(max(int(nws), 1), dtype=torch.uint8, device=Q.device)
+    _check(L.fa_dense_bwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(dO), _ptr(l), _ptr(m),
+                          _ptr(dQ), _ptr(dK), _ptr(dV), N, Nk, d, dv, B, float(scale),
+                          _ptr(ws), int(nws), _stream(Q)))
+    return dQ, dK, dV
+
+
+# ----------------------------------------------------------------------------
+# windowed
+# ----------------------------------------------------------------------------
+def window_geometry(spatial: Sequence[int], ws: int, stride: int, pad: int):
+    """Windows per spatial dim of NNlib.unfold (src/utils.jl:40)."""
+    out = tuple((s + 2 * pad - ws) // stride + 1 for s in spatial)
+    _require(all(o >= 1 for o in out), "window larger than the padded input")
+    return out
+
+
+def _i64_array(xs):
+    arr = (ctypes.c_int64 * len(xs))(*[int(x) for x in xs])
+    return arr
+
+
+def windowed_fa(q, k, v, windowsize: int, stride: Optional[int] = None,
+                pad: Optional[int] = None, scale: float = 0.0):
+    """``windowed_fa(q, k, v, ws; stride=ws, pad=(ws-1)÷2) -> (y, l, m)`` —
+    src/windowed.jl:3-23, fused on the device.
+
+    q, k: (S..., d, B); v: (S..., dv, B); y: (S..., dv, B) with NaN where no
+    window covers a pixel (as the reference); l, m: (ws^k, 1, L, B) float32.
+    """
+    stride = windowsize if stride is None else int(stride)
+    pad = (windowsize - 1) // 2 if pad is None else int(pad)
+    D = q.dim()
+    _require(D >= 3 and k.dim() == D and v.dim() == D, "q, k, v must share rank >= 3")
+    nsp = D - 2
+    _require(1 <= nsp <= 3, "1 to 3 spatial dims supported")
+    sp = tuple(q.shape[:nsp])
+    d, B = q.shape[D - 2], q.shape[D - 1]
+    dv = v.shape[D - 2]
+    _require(tuple(k.shape) == tuple(q.shape), "k must have q's shape")
+    _require(tuple(v.shape[:nsp]) == sp and v.shape[D - 1] == B, "v must share q's spatial dims and batch")
+    outs = window_geometry(sp, windowsize, stride, pad)
+    code = _dtype_code(q, k, v)
+    _device_check(q, k, v)
+    T = windowsize ** nsp
+    L = math.prod(outs)
+    y = jl_empty(sp + (dv, B), q.dtype, q.device)
+    lw = jl_empty((T, 1, L, B), torch.float32, q.device)
+    mw = jl_empty((T, 1, L, B), torch.float32, q.device)
+    _check(lib().fa_windowed_fwd(code, _ptr(q), _ptr(k), _ptr(v), _ptr(y), _ptr(lw), _ptr(mw),
+                                 nsp, _i64_array(sp), d, dv, B, windowsize, stride, pad,
+                                 float(scale), _stream(q)))
+    return y, lw, mw
+
+
+def block_fa(q, k, v, windowsize: int, pad: int = 0, scale: float = 0.0):
+    """``block_fa(q, k, v, ws; pad=0)`` = windowed_fa with stride = ws — src/windowed.jl:1."""
+    return windowed_fa(q, k, v, windowsize, stride=windowsize, pad=pad, scale=scale)
+
+
+def windowed_fa_backward(q, k, v, y, dy, l, m, windowsize: int, stride: Optional[int] = None,
+                         pad: Optional[int] = None, scale: float = 0.0):
+    """Backward of :func:`windowed_fa`: returns (dq, dk, dv)."""
+    stride = windowsize if stride is None else int(stride)
+    pad = (windowsize - 1) // 2 if pad is None else int(pad)
+    D = q.dim()
+    nsp = D - 2
+    sp = tuple(q.shape[:nsp])
+    d, B = q.shape[D - 2], q.shape[D - 1]
+    dv = v.shape[D - 2]
+    code = _dtype_code(q, k, v, y, dy)
+    _device_check(q, k, v, y, dy, l, m)
+    dq = jl_empty(sp + (d, B), q.dtype, q.device)
+    dk = jl_empty(sp + (d, B), q.dtype, q.device)
+    dvv = jl_empty(sp + (dv, B), q.dtype, q.device)
+    Lb = lib()
+    spa = _i64_array(sp)
+    nws = Lb.fa_windowed_workspace(code, nsp, spa, d, dv, B, windowsize, stride, pad)
+    ws = torch.empty(max(int(nws), 1), dtype=torch.uint8, device=q.device)
+    _check(Lb.fa_windowed_bwd(code, _ptr(q), _ptr(k), _ptr(v), _ptr(y), _ptr(dy), _ptr(l), _ptr(m),
+                              _ptr(dq), _ptr(dk), _ptr(dvv), nsp, spa, d, dv, B, windowsize,
+                              stride, pad, float(scale), _ptr(ws), int(nws), _stream(q)))
+    return dq, dk, dvv

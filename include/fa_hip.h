@@ -1,0 +1,137 @@
+/*
+ * fa_hip.h — C ABI of the MI355X (gfx950) flash-attention library.
+ *
+ * Drop-in boundary for the hot path of nikopj/FlashAttention.jl
+ * (reference mounted read-only at /root/reference; citations are path:line
+ * inside it).  The Julia host code binds these symbols with `ccall`
+ * (INTEGRATION.md); the Python ctypes mirror in flashattention.jl_amd/fa_hip
+ * binds the very same symbols, so parity evidence transfers.
+ *
+ * Layout contract (all entry points): the reference's Julia column-major
+ * layout with contiguous batch.  A 3-D array X of Julia shape (N, d, B) sits
+ * at element offset  n + N*k + N*d*b  (src/dense.jl:6-8 flattens spatial dims
+ * into N).  l and m are (N, 1, B): offset n + N*b.  There is no separate head
+ * dimension: (batch, heads) of the benchmark configs are one batch of B*H
+ * (SURVEY.md §8a).
+ *
+ * Every pointer is a DEVICE pointer owned by the caller.  Inputs are read
+ * only; outputs are fully written (the callee initialises, as
+ * src/dense.jl:58-60 does).  `hip_stream` is a hipStream_t (NULL = default
+ * stream).  Calls are asynchronous on that stream, stateless, and safe from
+ * concurrent host threads on distinct streams.  No call allocates device
+ * memory, synchronises, or aborts: each returns FA_OK (0) or a nonzero
+ * fa_status, with a thread-local message in fa_last_error().
+ */
+#ifndef FA_HIP_H
+#define FA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_HIP_ABI_VERSION 1
+
+/* Element type of Q, K, V, O (and dO, dQ, dK, dV).  l, m are always float32
+ * (documented deviation for 16-bit types: the reference keeps them in T,
+ * src/dense.jl:12-13). */
+typedef enum fa_dtype {
+    FA_DTYPE_F32  = 0,
+    FA_DTYPE_BF16 = 1,
+    FA_DTYPE_F16  = 2
+} fa_dtype;
+
+typedef enum fa_status {
+    FA_OK                = 0,
+    FA_ERR_INVALID_ARG   = 1, /* bad pointer / size / dtype (reference: DimensionMismatch) */
+    FA_ERR_UNSUPPORTED   = 2, /* valid but unsupported (e.g. head dim > fa_max_head_dim()) */
+    FA_ERR_HIP           = 3, /* HIP launch / runtime error */
+    FA_ERR_WORKSPACE     = 4  /* workspace missing or too small */
+} fa_status;
+
+/* Dense forward.  Replaces the body of
+ *   dense_fa!(O, l, m, Q, K, V)          src/dense.jl:21-102
+ * (and, with caller-side allocation, dense_fa(q, k, v), src/dense.jl:1-19).
+ *   Q (N, d, B), K (Nk, d, B), V (Nk, dv, B)  ->  O (N, dv, B),
+ *   l (N, 1, B) = sum_j exp(s_ij - m_i),  m (N, 1, B) = max_j s_ij,
+ *   s = scale * Q K^T  (natural-log units, as src/dense.jl:78-91).
+ * scale <= 0 selects the reference's tau = 1/sqrt(d) (src/dense.jl:43).
+ * The reference requires Nk == N and dv == d (Appendix A.1); both are lifted. */
+int fa_dense_fwd(int dtype,
+                 const void* Q, const void* K, const void* V,
+                 void* O, float* l, float* m,
+                 int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
+                 float scale, void* hip_stream);
+
+/* Workspace bytes fa_dense_bwd needs for these sizes (0 is a valid answer). */
+size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
+                              int64_t dv, int64_t batch);
+
+/* Dense backward.  Replaces dense_fa_backward(Q, K, V, O, dO, l, m)
+ * (src/dense.jl:104-167; executable spec OneDFastBack,
+ * src_cpp/FlashAttention.cpp:194-252):
+ *   P = exp(s - m)/l, dV = P^T dO, dP = dO V^T, D = rowsum(dO .* O),
+ *   dS = P .* (dP - D), dQ = scale dS K, dK = scale dS^T Q.
+ * l, m are the forward's outputs.  dQ, dK, dV are fully written. */
+int fa_dense_bwd(int dtype,
+                 const void* Q, const void* K, const void* V,
+                 const void* O, const void* dO,
+                 const float* l, const float* m,
+                 void* dQ, void* dK, void* dV,
+                 int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
+                 float scale, void* workspace, size_t workspace_bytes,
+                 void* hip_stream);
+
+/* Windowed forward.  Replaces windowed_fa(q, k, v, ws; stride, pad)
+ * (src/windowed.jl:3-23; block_fa = stride ws, src/windowed.jl:1), fusing
+ * window (src/utils.jl:36-44) -> dense_fa -> unwindow / divisor
+ * (src/utils.jl:46-54, src/windowed.jl:16-19) into one pass.
+ *   q, k: (S_1, ..., S_k, d, B);  v: (S_1, ..., S_k, dv, B)
+ *   y:    (S_1, ..., S_k, dv, B)  (pixels no window covers are NaN, as in
+ *                                  the reference, Appendix A.7)
+ *   l, m: (ws^k, 1, L, B) window layout (src/windowed.jl:20-21),
+ *         L = prod_i ((S_i + 2 pad - ws) / stride + 1).
+ * nspatial = k in 1..3; pad < 0 selects the reference default (ws-1)/2. */
+int fa_windowed_fwd(int dtype,
+                    const void* q, const void* k, const void* v,
+                    void* y, float* l, float* m,
+                    int nspatial, const int64_t* spatial,
+                    int64_t d, int64_t dv, int64_t batch,
+                    int64_t ws, int64_t stride, int64_t pad,
+                    float scale, void* hip_stream);
+
+/* Workspace for fa_windowed_fwd / fa_windowed_bwd (bytes; 0 is valid). */
+size_t fa_windowed_workspace(int dtype, int nspatial, const int64_t* spatial,
+                             int64_t d, int64_t dv, int64_t batch,
+                             int64_t ws, int64_t stride, int64_t pad);
+
+/* Windowed backward (README.md:36-37 claims it, no code
+ * exists in the reference): the exact chain rule of windowed_fa.
+ * y, l, m are fa_windowed_fwd's outputs; dq, dk, dv fully written. */
+int fa_windowed_bwd(int dtype,
+                    const void* q, const void* k, const void* v,
+                    const void* y, const void* dy,
+                    const float* l, const float* m,
+                    void* dq, void* dk, void* dv_,
+                    int nspatial, const int64_t* spatial,
+                    int64_t d, int64_t dv, int64_t batch,
+                    int64_t ws, int64_t stride, int64_t pad,
+                    float scale, void* workspace, size_t workspace_bytes,
+                    void* hip_stream);
+
+/* Thread-local description of the last error on this host thread ("" if none). */
+const char* fa_last_error(void);
+
+/* FA_HIP_ABI_VERSION of the loaded library. */
+int fa_abi_version(void);
+
+/* Largest d (and dv) the kernels accept. */
+int fa_max_head_dim(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FA_HIP_H */

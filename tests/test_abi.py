@@ -1,0 +1,129 @@
+"""CPU tests of the C-ABI boundary: libfa_hip.so loads, exports every symbol
+include/fa_hip.h declares, and rejects bad arguments with the documented
+status codes and thread-local messages BEFORE touching the device (so these
+run without a GPU).  Plus the Python mirror's argument checking."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "fa_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(fa_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ("fa_dense_fwd", "fa_dense_bwd", "fa_dense_bwd_workspace", "fa_windowed_fwd",
+              "fa_windowed_bwd", "fa_windowed_workspace", "fa_last_error", "fa_abi_version",
+              "fa_max_head_dim"):
+        assert f in fns
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    import fa_hip
+    L = fa_hip.lib()
+    for f in declared_functions():
+        assert hasattr(L, f), f"{f} declared in fa_hip.h but not exported"
+    assert L.fa_abi_version() == 1
+    assert L.fa_max_head_dim() == 128
+
+
+def test_exports_are_c_symbols_not_mangled():
+    import subprocess
+    import fa_hip
+    out = subprocess.run(["nm", "-D", "--defined-only", fa_hip.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    for f in declared_functions():
+        assert f in syms
+
+
+def _i(x):
+    return ctypes.c_int64(x)
+
+
+def test_invalid_arguments_return_status_and_message():
+    import fa_hip
+    L = fa_hip.lib()
+    P = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    # unknown dtype
+    rc = L.fa_dense_fwd(9, P, P, P, P, P, P, 4, 4, 4, 4, 1, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"dtype" in L.fa_last_error()
+    # non-positive sizes → DimensionMismatch
+    rc = L.fa_dense_fwd(1, P, P, P, P, P, P, 0, 4, 4, 4, 1, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"DimensionMismatch" in L.fa_last_error()
+    # null pointer
+    rc = L.fa_dense_fwd(1, None, P, P, P, P, P, 4, 4, 4, 4, 1, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"null" in L.fa_last_error()
+    # unsupported head dim
+    rc = L.fa_dense_fwd(1, P, P, P, P, P, P, 4, 4, 129, 4, 1, 0.0, None)
+    assert rc == fa_hip.FA_ERR_UNSUPPORTED and b"head dimension" in L.fa_last_error()
+    # windowed: window larger than padded input
+    sp = (ctypes.c_int64 * 2)(5, 5)
+    rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 2, sp, 4, 4, 1, 9, 9, 0, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"window" in L.fa_last_error()
+    rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 4, sp, 4, 4, 1, 3, 3, 0, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"nspatial" in L.fa_last_error()
+    # backward: workspace check happens before any launch
+    need = L.fa_dense_bwd_workspace(1, 128, 128, 64, 64, 2)
+    if need > 0:
+        rc = L.fa_dense_bwd(1, P, P, P, P, P, P, P, P, P, P, 128, 128, 64, 64, 2, 0.0, None, 0, None)
+        assert rc == fa_hip.FA_ERR_WORKSPACE
+
+
+def test_last_error_is_thread_local():
+    import fa_hip
+    L = fa_hip.lib()
+    P = ctypes.c_void_p(16)
+    assert L.fa_dense_fwd(9, P, P, P, P, P, P, 4, 4, 4, 4, 1, 0.0, None) != 0
+    seen = {}
+
+    def other():
+        seen["msg"] = L.fa_last_error()
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen["msg"] == b""
+    assert b"dtype" in L.fa_last_error()
+
+
+def test_python_mirror_shape_checks_raise_dimension_mismatch():
+    import fa_hip
+    Q = fa_hip.jl_empty((8, 4, 2), device="cpu")
+    K = fa_hip.jl_empty((8, 5, 2), device="cpu")
+    O = fa_hip.jl_empty((8, 4, 2), device="cpu")
+    l = fa_hip.jl_empty((8, 1, 2), device="cpu")
+    with pytest.raises(fa_hip.DimensionMismatch):
+        fa_hip.dense_fa_(O, l, l, Q, K, Q)
+    with pytest.raises(fa_hip.DimensionMismatch):
+        fa_hip.dense_fa_(fa_hip.jl_empty((8, 3, 2), device="cpu"), l, l, Q, Q, Q)
+    # correct shapes but host arrays: loud refusal, no CPU fallback
+    with pytest.raises(TypeError, match="no CPU fallback"):
+        fa_hip.dense_fa_(O, l, l, Q, Q, Q)
+    with pytest.raises(fa_hip.DimensionMismatch):
+        fa_hip.windowed_fa(fa_hip.jl_empty((4, 4, 2, 1), device="cpu"),
+                           fa_hip.jl_empty((4, 4, 2, 1), device="cpu"),
+                           fa_hip.jl_empty((4, 4, 2, 1), device="cpu"), 9, stride=9, pad=0)
+
+
+def test_julia_layout_helpers():
+    import fa_hip
+    t = fa_hip.jl_empty((5, 3, 2), device="cpu")
+    assert t.shape == (5, 3, 2) and t.stride() == (1, 5, 15)
+    assert fa_hip.is_jl_contiguous(t)
+    assert not fa_hip.is_jl_contiguous(torch.empty(5, 3, 2))
+    x = torch.arange(30.0).reshape(5, 3, 2)
+    assert torch.equal(fa_hip.jl_tensor(x, device="cpu"), x)

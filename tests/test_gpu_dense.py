@@ -1,0 +1,187 @@
+"""GPU parity tests: dense forward through the C ABI (fa_dense_fwd) vs the
+float64 oracle (oracle/fa_oracle.py) on the committed golden vectors, edge
+cases the reference exercises or breaks on, and size-independent properties
+at BASELINE.json's full sizes.  Tolerances: tests/conftest.py."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close, assert_lm_close, golden_files, load_golden
+from oracle import fa_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DT = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
+
+
+@pytest.fixture(scope="module")
+def fa():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    import fa_hip
+    fa_hip.lib()
+    return fa_hip
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+@pytest.mark.parametrize("dtype", list(DT))
+@pytest.mark.parametrize("path", golden_files("dense_"), ids=lambda p: p.split("/")[-1][:-4])
+def test_dense_golden(fa, path, dtype):
+    g = load_golden(path)
+    q, k, v = (fa.jl_tensor(g[x], DT[dtype]) for x in ("q", "k", "v"))
+    y, l, m = fa.dense_fa(q, k, v)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == g["y"].shape and fa.is_jl_contiguous(y)
+    assert_close(_np(y), g["y"], dtype, "y")
+    assert_lm_close(_np(l), g["l"], dtype, "l")
+    assert_lm_close(_np(m), g["m"], dtype, "m")
+
+
+def test_reference_test_jl_shape_against_dpa(fa):
+    """test/test.jl:5-21: dense_fa ≈ dense_dpa with Nq = Nkv = 30, dqk = 12, dv = 6
+    (the reference itself throws DimensionMismatch here, Appendix A.1)."""
+    rng = np.random.default_rng(0)
+    q, k, v = rng.random((30, 12, 2)), rng.random((30, 12, 2)), rng.random((30, 6, 2))
+    y, l, m = fa.dense_fa(*(fa.jl_tensor(a, torch.float32) for a in (q, k, v)))
+    y1, _ = O.dense_dpa(q.astype(np.float32), k.astype(np.float32), v.astype(np.float32))
+    # Julia ≈ : norm(x - y) <= sqrt(eps(T)) * max(norm(x), norm(y))
+    assert np.linalg.norm(_np(y) - y1) <= math.sqrt(np.finfo(np.float32).eps) * np.linalg.norm(y1)
+
+
+def test_inplace_overwrites_every_output(fa):
+    """dense_fa! semantics: callee initialises O, l, m (src/dense.jl:58-60)."""
+    rng = np.random.default_rng(1)
+    N, Nk, d, dv, B = 200, 190, 64, 64, 3
+    q, k, v = rng.standard_normal((N, d, B)), rng.standard_normal((Nk, d, B)), rng.standard_normal((Nk, dv, B))
+    Q, K, V = (fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v))
+    Ob = fa.jl_empty((N, dv, B), torch.bfloat16); Ob.fill_(float("nan"))
+    lb = fa.jl_empty((N, 1, B)); lb.fill_(float("nan"))
+    mb = fa.jl_empty((N, 1, B)); mb.fill_(float("nan"))
+    r = fa.dense_fa_(Ob, lb, mb, Q, K, V)
+    assert r[0] is Ob and r[1] is lb and r[2] is mb
+    torch.cuda.synchronize()
+    yr, lr, mr = O.dense_fa3(_np(Q), _np(K), _np(V))
+    assert_close(_np(Ob), yr, "bfloat16", "O")
+    assert_lm_close(_np(lb), lr, "bfloat16", "l")
+    assert_lm_close(_np(mb), mr, "bfloat16", "m")
+
+
+@pytest.mark.parametrize("N,Nk,d,dv,B", [(1, 1, 64, 64, 1), (1, 300, 64, 64, 2), (300, 1, 64, 64, 2),
+                                         (65, 63, 16, 8, 2), (129, 257, 128, 128, 1), (127, 65, 128, 32, 2),
+                                         (33, 4100, 64, 64, 1), (3, 7, 1, 1, 2), (70, 70, 33, 65, 1)])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_ragged_and_tiny_shapes(fa, N, Nk, d, dv, B, dtype):
+    """Ragged N / Nk (keys masked to -inf, not zero-filled: Appendix A.4),
+    Nk != N and dv != d (lifted reference restrictions), head-dim padding."""
+    rng = np.random.default_rng(N * 1000 + Nk)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    q, k, v = bf(rng.standard_normal((N, d, B))), bf(rng.standard_normal((Nk, d, B))), bf(rng.standard_normal((Nk, dv, B)))
+    y, l, m = fa.dense_fa(*(fa.jl_tensor(a, DT[dtype]) for a in (q, k, v)))
+    yr, lr, mr = O.dense_fa3(q, k, v)
+    torch.cuda.synchronize()
+    assert_close(_np(y), yr, dtype, "y")
+    assert_lm_close(_np(l), lr, dtype, "l")
+    assert_lm_close(_np(m), mr, dtype, "m")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_running_max_rescale_branch(fa, dtype):
+    """Force the online-softmax rescale at chosen tiles (cdna guide rule 26):
+    a spike key whose score jumps far above every earlier tile's max, placed
+    in the 3rd and 9th key tiles, for a subset of query rows."""
+    rng = np.random.default_rng(7)
+    N, Nk, d, B = 256, 640, 64, 2
+    q = rng.standard_normal((N, d, B)) * 0.5
+    k = rng.standard_normal((Nk, d, B)) * 0.5
+    v = rng.standard_normal((Nk, d, B))
+    k[150] = q[10] * 6.0
+    k[560] = q[200] * 8.0
+    k[600, :, 1] = -q[100, :, 1] * 8.0
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    q, k, v = bf(q), bf(k), bf(v)
+    y, l, m = fa.dense_fa(*(fa.jl_tensor(a, DT[dtype]) for a in (q, k, v)))
+    yr, lr, mr = O.dense_fa3(q, k, v)
+    torch.cuda.synchronize()
+    assert_close(_np(y), yr, dtype, "y")
+    assert_lm_close(_np(m), mr, dtype, "m")
+    assert_lm_close(_np(l), lr, dtype, "l")
+
+
+def test_explicit_scale_and_nondefault_stream(fa):
+    rng = np.random.default_rng(9)
+    N, d, B = 130, 32, 2
+    q, k, v = (rng.standard_normal((N, d, B)) for _ in range(3))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        y, l, m = fa.dense_fa(*(fa.jl_tensor(a, torch.float32) for a in (q, k, v)), scale=0.3)
+    s.synchronize()
+    # reference math with tau replaced by 0.3 ≡ oracle on q scaled by 0.3*sqrt(d)
+    yr, lr, mr = O.dense_fa3(q * 0.3 * math.sqrt(d), k, v)
+    assert_close(_np(y), yr, "float32", "y")
+    assert_lm_close(_np(m), mr, "float32", "m")
+
+
+def test_deterministic(fa):
+    rng = np.random.default_rng(10)
+    q, k, v = (fa.jl_tensor(rng.standard_normal((1000, 64, 4)), torch.bfloat16) for _ in range(3))
+    a = fa.dense_fa(q, k, v)
+    b = fa.dense_fa(q, k, v)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def _full_size_properties(fa, N, d, BH, dtype, check_slabs=(0,)):
+    """BASELINE config at full size: oracle on a few slabs + size-independent
+    properties on all slabs."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    Q = fa.jl_empty((N, d, BH), dtype); Q.copy_(torch.randn(Q.shape, generator=g, device="cuda"))
+    K = fa.jl_empty((N, d, BH), dtype); K.copy_(torch.randn(K.shape, generator=g, device="cuda"))
+    V = fa.jl_empty((N, d, BH), dtype); V.copy_(torch.randn(V.shape, generator=g, device="cuda"))
+    y, l, m = fa.dense_fa(Q, K, V)
+    torch.cuda.synchronize()
+    # (1) oracle on selected slabs
+    for b in check_slabs:
+        yr, lr, mr = O.dense_fa3(_np(Q[:, :, b:b + 1]), _np(K[:, :, b:b + 1]), _np(V[:, :, b:b + 1]))
+        assert_close(_np(y[:, :, b:b + 1]), yr, "bfloat16", f"y slab {b}")
+        assert_lm_close(_np(l[:, :, b:b + 1]), lr, "bfloat16", f"l slab {b}")
+        assert_lm_close(_np(m[:, :, b:b + 1]), mr, "bfloat16", f"m slab {b}")
+    yf = y.float()
+    # (2) convex combination: min_j V <= O <= max_j V per feature and slab
+    vmin = V.float().amin(0, keepdim=True); vmax = V.float().amax(0, keepdim=True)
+    tol = 1e-2 * (1 + vmax.abs())
+    assert bool(((yf >= vmin - tol) & (yf <= vmax + tol)).all())
+    # (3) 1 <= l <= Nk
+    assert bool(((l >= 1 - 1e-4) & (l <= N * (1 + 1e-4))).all())
+    # (4) affine equivariance: softmax rows sum to one, so V -> 2V + 1 gives 2O + 1
+    V2 = fa.jl_empty(V.shape, dtype); V2.copy_(2 * V.float() + 1)
+    y2, _, m2 = fa.dense_fa(Q, K, V2)
+    torch.cuda.synchronize()
+    assert torch.allclose(y2.float(), 2 * yf + 1, atol=4e-2, rtol=2e-2)
+    assert torch.equal(m2, m)
+    # (5) key permutation invariance (K and V tokens permuted together)
+    perm = torch.randperm(N, generator=torch.Generator().manual_seed(3)).cuda()
+    Kp = fa.jl_empty(K.shape, dtype); Kp.copy_(K[perm])
+    Vp = fa.jl_empty(V.shape, dtype); Vp.copy_(V[perm])
+    y3, l3, m3 = fa.dense_fa(Q, Kp, Vp)
+    torch.cuda.synchronize()
+    assert torch.allclose(y3.float(), yf, atol=2e-2, rtol=2e-2)
+    assert torch.allclose(m3, m, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(l3, l, rtol=1e-4)
+
+
+def test_config2_full_size_properties(fa):
+    """BASELINE configs[1]: (B,H,N,d) = (4,16,4096,64) bf16 → (N, d, B·H) = (4096, 64, 64)."""
+    _full_size_properties(fa, 4096, 64, 64, torch.bfloat16, check_slabs=(0, 37, 63))
+
+
+def test_config4_full_size_forward_properties(fa):
+    """BASELINE configs[3] forward: (4,16,8192,128) bf16 → (8192, 128, 64)."""
+    _full_size_properties(fa, 8192, 128, 64, torch.bfloat16, check_slabs=(5,))
