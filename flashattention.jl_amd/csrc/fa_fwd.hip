@@ -89,7 +89,7 @@ __device__ __forceinline__ u32x4 load_chunk(const T* base, int row, int col0, in
 // bf16 / fp16 forward (v_mfma_f32_32x32x16_{bf16,f16})
 // --------------------------------------------------------------------------
 template <class T, int D, int DV>
-__global__ __launch_bounds__(kThreads) void dense_fwd_mfma16(FwdParams p) {
+__global__ __launch_bounds__(kThreads) void dense_fwd_generic(FwdParams p) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
     constexpr int KROW = kBN * 2;       // K image: [D][64 keys], 128-B rows, 32-B chunk XOR swizzle
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kThreads) void dense_fwd_mfma16(FwdParams p) {
 // fp32 forward (exact f32 MFMA v_mfma_f32_32x32x2_f32)
 // --------------------------------------------------------------------------
 template <int D, int DV>
-__global__ __launch_bounds__(kThreads) void dense_fwd_f32(FwdParams p) {
+__global__ __launch_bounds__(kThreads) void dense_fwd_generic_f32(FwdParams p) {
     constexpr int KROWF = kBN;       // K image [D][64] floats
     constexpr int VROWF = kBN + 1;   // V image [DV][65] floats (pad → conflict-free column reads)
     constexpr int KCH = D * 16 / kThreads;
@@ -431,14 +431,237 @@ __global__ __launch_bounds__(kThreads) void dense_fwd_f32(FwdParams p) {
 }
 
 // --------------------------------------------------------------------------
+// bf16 / fp16 fast path: K/V rows 16-B aligned, Nk % 8 == 0, slab < 4 GiB.
+//
+// Differences from the generic kernel:
+//  * every global access is an unconditional buffer load through a per-slab
+//    descriptor (num_records = slab bytes): reads of padded feature rows
+//    (f >= d) fall outside the slab and return 0, so the loop body has no
+//    divergent control flow and hipcc keeps the tile loads in flight across the
+//    whole compute phase (no vmcnt(0) next to the issue);
+//  * LDS is double-buffered: tile j+1's registers are written into the other
+//    buffer right after tile j's compute, one barrier per tile;
+//  * lazy rescaling: the running max used for the exponentials (m_used) is
+//    only raised when a tile's max exceeds it by more than kRescaleLog2 (in
+//    log2 units), so the O / l rescale is a rare, wave-uniform branch; P is then
+//    bounded by 2^kRescaleLog2 (bf16 keeps its relative precision), and the
+//    exact max is tracked separately for the returned m (and l is converted to
+//    it at the end).
+// --------------------------------------------------------------------------
+constexpr float kRescaleLog2 = 8.0f;
+
+template <class T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const T* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(kThreads, 2) void dense_fwd_fast(FwdParams p) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int KROW = kBN * 2;
+    constexpr int VROW = kBN * 2 + 16;
+    constexpr int KBYTES = D * KROW, VBYTES = DV * VROW, STAGE = KBYTES + VBYTES;
+    constexpr int KCH = D * 8 / kThreads;
+    constexpr int VCH = DV * 8 / kThreads;
+    static_assert(KCH >= 1 && VCH >= 1, "head dim class too small");
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int lid = xcd_remap(blockIdx.x, p.total_wg);
+    const int b = lid / p.nqb;
+    const int qb = lid - b * p.nqb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
+    const auto qrs = slab_rsrc((const T*)p.Q + (int64_t)b * N * d, (uint32_t)(N * d * (int)sizeof(T)));
+    const auto krs = slab_rsrc((const T*)p.K + (int64_t)b * Nk * d, (uint32_t)(Nk * d * (int)sizeof(T)));
+    const auto vrs = slab_rsrc((const T*)p.V + (int64_t)b * Nk * dv, (uint32_t)(Nk * dv * (int)sizeof(T)));
+
+    const int qi = qb * kBM + wave * 32 + r;
+    F8 qf[D / 16];
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int f = 16 * s + 8 * h + e;
+            const unsigned short u = __builtin_amdgcn_raw_buffer_load_b16(qrs, (f * N + qi) * 2, 0, 0);
+            qf[s][e] = __builtin_bit_cast(T, u);
+        }
+
+    const int g = lane >> 4, kh = g & 1, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    int koff[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+        koff[kb] = (8 * h + qq) * KROW + (((kb * 2 + kh) ^ (((qq >> 1) & 1) << 1)) * 32) + 8 * sig;
+    const int voff = r * VROW + 16 * h;
+
+    // per-thread global offsets (bytes) and LDS store offsets of its chunks
+    int kgo[KCH], kso[KCH], vgo[VCH], vso[VCH];
+#pragma unroll
+    for (int it = 0; it < KCH; ++it) {
+        const int ch = tid + kThreads * it, f = ch >> 3, pc = ch & 7;
+        kgo[it] = (f * Nk + pc * 8) * 2;
+        kso[it] = f * KROW + (((pc >> 1) ^ (((f >> 1) & 1) << 1)) * 32) + (pc & 1) * 16;
+    }
+#pragma unroll
+    for (int it = 0; it < VCH; ++it) {
+        const int ch = tid + kThreads * it, f = ch >> 3, pc = ch & 7;
+        vgo[it] = (f * Nk + pc * 8) * 2;
+        vso[it] = f * VROW + pc * 16;
+    }
+    const int my_key8 = (tid & 7) * 8;  // first key of this thread's chunks within a tile
+
+    f32x16 oacc[DV / 32];
+#pragma unroll
+    for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) oacc[cb][x] = 0.0f;
+    float m_used = kNegInf, m_true = kNegInf, l_run = 0.0f;
+    const float c = p.scale_log2;
+    const float thr_raw = kRescaleLog2 / c;
+
+    u32x4 kreg[KCH], vreg[VCH];
+    auto gload = [&](int j) {
+        const int kb0 = j * kBN * 2;
+#pragma unroll
+        for (int it = 0; it < KCH; ++it) kreg[it] = __builtin_amdgcn_raw_buffer_load_b128(krs, kgo[it] + kb0, 0, 0);
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) vreg[it] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vgo[it] + kb0, 0, 0);
+        // keys >= Nk (partial last tile) read the next feature row: zero V there so
+        // that P = 0 meets a finite value (K is masked to -inf on the scores).
+        const bool dead = j * kBN + my_key8 >= Nk;
+#pragma unroll
+        for (int it = 0; it < VCH; ++it)
+            if (dead) vreg[it] = u32x4{0u, 0u, 0u, 0u};
+    };
+    auto lstore = [&](char* buf) {
+#pragma unroll
+        for (int it = 0; it < KCH; ++it) *(u32x4*)(buf + kso[it]) = kreg[it];
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) *(u32x4*)(buf + KBYTES + vso[it]) = vreg[it];
+    };
+
+    auto compute = [&](const char* klds, const char* vlds, int j) {
+        f32x16 sacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sacc[kb][x] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) {
+                const char* a = klds + koff[kb] + 16 * s * KROW;
+                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW));
+                const F8 af = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                sacc[kb] = mfma32x32x16(af, qf[s], sacc[kb]);
+            }
+        }
+        const int key0 = j * kBN;
+        if (key0 + kBN > Nk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) {
+                    const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+                    if (key0 + kt >= Nk) sacc[kb][x] = kNegInf;
+                }
+        }
+        float mt = kNegInf;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) mt = fmaxf(mt, sacc[kb][x]);
+        mt = swap_halves_max(mt);
+        m_true = fmaxf(m_true, mt);
+        if (__builtin_amdgcn_ballot_w64(mt > m_used + thr_raw) != 0) {   // wave-uniform, rare
+            const float m_new = fmaxf(m_used, mt);
+            const float alpha = exp2_fast((m_used - m_new) * c);
+            l_run *= alpha;
+#pragma unroll
+            for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) oacc[cb][x] *= alpha;
+            m_used = m_new;
+        }
+        const float mc = m_used * c;
+        float ls = 0.0f;
+        F8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pv = exp2_fast(fmaf(sacc[kb][x], c, -mc));
+                ls += pv;
+                pf[kb][x >> 3][x & 7] = (T)pv;
+            }
+        l_run += ls;
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const F8 va = *(const F8*)(vlds + voff + cb * 32 * VROW + (kb * 32 + 16 * s) * 2);
+                    oacc[cb] = mfma32x32x16(va, pf[kb][s], oacc[cb]);
+                }
+    };
+
+    const int ntiles = (Nk + kBN - 1) / kBN;
+    char* const buf0 = smem;
+    char* const buf1 = smem + STAGE;
+    gload(0);
+    lstore(buf0);
+    __syncthreads();
+    for (int j = 0; j < ntiles; j += 2) {
+        gload(min(j + 1, ntiles - 1));
+        compute(buf0, buf0 + KBYTES, j);
+        lstore(buf1);
+        __syncthreads();
+        if (j + 1 < ntiles) {
+            gload(min(j + 2, ntiles - 1));
+            compute(buf1, buf1 + KBYTES, j + 1);
+            lstore(buf0);
+            __syncthreads();
+        }
+    }
+
+    const float lt = swap_halves_sum(l_run);
+    const float inv = 1.0f / lt;
+    if (qi < N) {
+        T* Ob = (T*)p.O + (int64_t)b * N * dv;
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = cb * 32 + acc_row(x, h);
+                if (cc < dv) Ob[(int64_t)cc * N + qi] = (T)(oacc[cb][x] * inv);
+            }
+        if (h == 0) {
+            p.m[(int64_t)b * N + qi] = m_true * p.scale;
+            p.l[(int64_t)b * N + qi] = lt * exp2_fast((m_used - m_true) * c);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
 template <class T, int D>
 static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
+    if (p.fast) {
+        switch (DVc) {
+            case 32: hipLaunchKernelGGL((dense_fwd_fast<T, D, 32>), grid, dim3(kThreads), 0, s, p); break;
+            case 64: hipLaunchKernelGGL((dense_fwd_fast<T, D, 64>), grid, dim3(kThreads), 0, s, p); break;
+            case 128: hipLaunchKernelGGL((dense_fwd_fast<T, D, 128>), grid, dim3(kThreads), 0, s, p); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (DVc) {
-        case 32: hipLaunchKernelGGL((dense_fwd_mfma16<T, D, 32>), grid, dim3(kThreads), 0, s, p); break;
-        case 64: hipLaunchKernelGGL((dense_fwd_mfma16<T, D, 64>), grid, dim3(kThreads), 0, s, p); break;
-        case 128: hipLaunchKernelGGL((dense_fwd_mfma16<T, D, 128>), grid, dim3(kThreads), 0, s, p); break;
+        case 32: hipLaunchKernelGGL((dense_fwd_generic<T, D, 32>), grid, dim3(kThreads), 0, s, p); break;
+        case 64: hipLaunchKernelGGL((dense_fwd_generic<T, D, 64>), grid, dim3(kThreads), 0, s, p); break;
+        case 128: hipLaunchKernelGGL((dense_fwd_generic<T, D, 128>), grid, dim3(kThreads), 0, s, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -446,9 +669,9 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
 template <int D>
 static hipError_t launch_dv_f32(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
     switch (DVc) {
-        case 32: hipLaunchKernelGGL((dense_fwd_f32<D, 32>), grid, dim3(kThreads), 0, s, p); break;
-        case 64: hipLaunchKernelGGL((dense_fwd_f32<D, 64>), grid, dim3(kThreads), 0, s, p); break;
-        case 128: hipLaunchKernelGGL((dense_fwd_f32<D, 128>), grid, dim3(kThreads), 0, s, p); break;
+        case 32: hipLaunchKernelGGL((dense_fwd_generic_f32<D, 32>), grid, dim3(kThreads), 0, s, p); break;
+        case 64: hipLaunchKernelGGL((dense_fwd_generic_f32<D, 64>), grid, dim3(kThreads), 0, s, p); break;
+        case 128: hipLaunchKernelGGL((dense_fwd_generic_f32<D, 128>), grid, dim3(kThreads), 0, s, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -498,6 +721,11 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     p.scale_log2 = a.scale * kLog2e;
     const int epc = a.dtype == FA_DTYPE_F32 ? 4 : 8;
     p.fast = (a.Nk % epc == 0) && aligned16(a.K) && aligned16(a.V);
+    // buffer descriptors address a slab with 32-bit byte offsets
+    const int64_t esz = a.dtype == FA_DTYPE_F32 ? 4 : 2;
+    if (a.N * a.d * esz >= (int64_t)INT32_MAX || a.Nk * a.d * esz >= (int64_t)INT32_MAX ||
+        a.Nk * a.dv * esz >= (int64_t)INT32_MAX)
+        p.fast = 0;
     const dim3 grid((unsigned)total);
     hipError_t e;
     switch (a.dtype) {
