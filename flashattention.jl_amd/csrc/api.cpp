@@ -73,6 +73,15 @@ int fa_abi_version(void) { return FA_HIP_ABI_VERSION; }
 
 int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
 
+// Not part of the public header: selects the forward kernel variant for A/B
+// benchmarking: 0 = auto (per head-dim class), 4..7 = {waves, query blocks per
+// wave} = {4,1}, {8,1}, {4,2}, {8,2}.
+int fa_debug_set_fwd_variant(int v) {
+    const int old = fa::g_fwd_variant;
+    if (v == 0 || (v >= 4 && v <= 7)) fa::g_fwd_variant = v;
+    return old;
+}
+
 int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
                  int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch, float scale,
                  void* hip_stream) {

@@ -40,11 +40,15 @@
 // fp32 inputs use the exact-f32 MFMA v_mfma_f32_32x32x2_f32 (no TF32 on
 // gfx950) with the same structure; that path exists for fp32 parity, the
 // performance path is bf16 / fp16.
+#include <type_traits>
+
 #include "fa_common.h"
 #include "fa_internal.h"
 #include "../../include/fa_hip.h"
 
 namespace fa {
+
+int g_fwd_variant = 0;  // 0: auto; 4..7: forced geometry (benchmark knob, fa_debug_set_fwd_variant)
 
 struct FwdParams {
     const void* Q;
@@ -450,22 +454,40 @@ __global__ __launch_bounds__(kThreads) void dense_fwd_generic_f32(FwdParams p) {
 // --------------------------------------------------------------------------
 constexpr float kRescaleLog2 = 8.0f;
 
+
 template <class T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const T* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }
 
-template <class T, int D, int DV>
-__global__ __launch_bounds__(kThreads, 2) void dense_fwd_fast(FwdParams p) {
+// --------------------------------------------------------------------------
+// bf16 / fp16 fast path, generalised geometry: NW waves x 32 query rows per
+// workgroup, BN keys per tile (the v2 structure: double-buffered LDS, one
+// barrier per tile, lazy rescale, branch-free buffer loads).  The partial-tile
+// V zeroing runs only on the last tile.
+// --------------------------------------------------------------------------
+template <class T, int D, int DV, int NW, int BN, int NQB>
+__device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
-    constexpr int KROW = kBN * 2;
-    constexpr int VROW = kBN * 2 + 16;
+    constexpr int NTH = 64 * NW;
+    constexpr int BM = 32 * NW * NQB;           // query rows per workgroup
+    constexpr int NKB = BN / 32;                // 32-key accumulator blocks per tile
+    constexpr int KROW = BN * 2;                // K image row (bytes)
+    constexpr int VROW = BN * 2 + 16;           // V image row (bytes), padded
     constexpr int KBYTES = D * KROW, VBYTES = DV * VROW, STAGE = KBYTES + VBYTES;
-    constexpr int KCH = D * 8 / kThreads;
-    constexpr int VCH = DV * 8 / kThreads;
-    static_assert(KCH >= 1 && VCH >= 1, "head dim class too small");
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    constexpr int CPR = BN / 8;                 // 16-B chunks per row
+    constexpr int KTOT = D * CPR, VTOT = DV * CPR;   // 16-B chunks per tile
+    constexpr int KCH = (KTOT + NTH - 1) / NTH;
+    constexpr int VCH = (VTOT + NTH - 1) / NTH;
+    static_assert(KTOT % NTH == 0 || KTOT < NTH, "tile split");
+    static_assert(VTOT % NTH == 0 || VTOT < NTH, "tile split");
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 16];   // +16: dump slot
+
+    // K image swizzle: XOR the 32-B chunk index so that the 4 feature rows a
+    // transposed read touches land on distinct banks (128-B rows: rows f and
+    // f+1 are 32 banks apart already; 256-B rows need a 2-bit XOR).
+    auto kswz = [](int f) { return BN == 64 ? (((f >> 1) & 1) << 1) : ((f & 3) << 1); };
 
     const int lid = xcd_remap(blockIdx.x, p.total_wg);
     const int b = lid / p.nqb;
@@ -477,172 +499,205 @@ __global__ __launch_bounds__(kThreads, 2) void dense_fwd_fast(FwdParams p) {
     const auto krs = slab_rsrc((const T*)p.K + (int64_t)b * Nk * d, (uint32_t)(Nk * d * (int)sizeof(T)));
     const auto vrs = slab_rsrc((const T*)p.V + (int64_t)b * Nk * dv, (uint32_t)(Nk * dv * (int)sizeof(T)));
 
-    const int qi = qb * kBM + wave * 32 + r;
-    F8 qf[D / 16];
+    int qiv[NQB];
+    F8 qf[NQB][D / 16];
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s)
+    for (int u = 0; u < NQB; ++u) {
+        qiv[u] = qb * BM + (wave * NQB + u) * 32 + r;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int f = 16 * s + 8 * h + e;
-            const unsigned short u = __builtin_amdgcn_raw_buffer_load_b16(qrs, (f * N + qi) * 2, 0, 0);
-            qf[s][e] = __builtin_bit_cast(T, u);
-        }
+        for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int f = 16 * s + 8 * h + e;
+                const unsigned short w = __builtin_amdgcn_raw_buffer_load_b16(qrs, (f * N + qiv[u]) * 2, 0, 0);
+                qf[u][s][e] = __builtin_bit_cast(T, w);
+            }
+    }
 
     const int g = lane >> 4, kh = g & 1, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
     const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-    int koff[2];
+    int koff[NKB];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-        koff[kb] = (8 * h + qq) * KROW + (((kb * 2 + kh) ^ (((qq >> 1) & 1) << 1)) * 32) + 8 * sig;
+    for (int kb = 0; kb < NKB; ++kb)
+        koff[kb] = (8 * h + qq) * KROW + (((kb * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
     const int voff = r * VROW + 16 * h;
 
-    // per-thread global offsets (bytes) and LDS store offsets of its chunks
     int kgo[KCH], kso[KCH], vgo[VCH], vso[VCH];
+    // threads past the chunk count (small head dims at 8 waves) load an
+    // out-of-range offset (→ 0) and store into a scratch slot past the tile
+    const bool kact = KTOT >= NTH || tid < KTOT, vact = VTOT >= NTH || tid < VTOT;
 #pragma unroll
     for (int it = 0; it < KCH; ++it) {
-        const int ch = tid + kThreads * it, f = ch >> 3, pc = ch & 7;
-        kgo[it] = (f * Nk + pc * 8) * 2;
-        kso[it] = f * KROW + (((pc >> 1) ^ (((f >> 1) & 1) << 1)) * 32) + (pc & 1) * 16;
+        const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
+        kgo[it] = kact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
+        kso[it] = kact ? f * KROW + (((pc >> 1) ^ kswz(f)) * 32) + (pc & 1) * 16 : 2 * STAGE;
     }
 #pragma unroll
     for (int it = 0; it < VCH; ++it) {
-        const int ch = tid + kThreads * it, f = ch >> 3, pc = ch & 7;
-        vgo[it] = (f * Nk + pc * 8) * 2;
-        vso[it] = f * VROW + pc * 16;
+        const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
+        vgo[it] = vact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
+        vso[it] = vact ? f * VROW + pc * 16 : 2 * STAGE - KBYTES;
     }
-    const int my_key8 = (tid & 7) * 8;  // first key of this thread's chunks within a tile
 
-    f32x16 oacc[DV / 32];
+    f32x16 oacc[NQB][DV / 32];
 #pragma unroll
-    for (int cb = 0; cb < DV / 32; ++cb)
+    for (int u = 0; u < NQB; ++u)
 #pragma unroll
-        for (int x = 0; x < 16; ++x) oacc[cb][x] = 0.0f;
-    float m_used = kNegInf, m_true = kNegInf, l_run = 0.0f;
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oacc[u][cb][x] = 0.0f;
+    float m_used[NQB], m_true[NQB], l_run[NQB];
+#pragma unroll
+    for (int u = 0; u < NQB; ++u) { m_used[u] = kNegInf; m_true[u] = kNegInf; l_run[u] = 0.0f; }
     const float c = p.scale_log2;
     const float thr_raw = kRescaleLog2 / c;
+    const int NT = (Nk + BN - 1) / BN;
+    const bool ragged = (Nk % BN) != 0;
 
     u32x4 kreg[KCH], vreg[VCH];
     auto gload = [&](int j) {
-        const int kb0 = j * kBN * 2;
+        const int kb0 = j * BN * 2;
 #pragma unroll
         for (int it = 0; it < KCH; ++it) kreg[it] = __builtin_amdgcn_raw_buffer_load_b128(krs, kgo[it] + kb0, 0, 0);
 #pragma unroll
         for (int it = 0; it < VCH; ++it) vreg[it] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vgo[it] + kb0, 0, 0);
-        // keys >= Nk (partial last tile) read the next feature row: zero V there so
-        // that P = 0 meets a finite value (K is masked to -inf on the scores).
-        const bool dead = j * kBN + my_key8 >= Nk;
-#pragma unroll
-        for (int it = 0; it < VCH; ++it)
-            if (dead) vreg[it] = u32x4{0u, 0u, 0u, 0u};
     };
-    auto lstore = [&](char* buf) {
+    auto lstore = [&](char* buf, int j) {
+        if (ragged && j == NT - 1) {   // keys >= Nk read the next feature row: zero V there
 #pragma unroll
-        for (int it = 0; it < KCH; ++it) *(u32x4*)(buf + kso[it]) = kreg[it];
+            for (int it = 0; it < VCH; ++it) {
+                const int ch = tid + NTH * it;
+                if (j * BN + (ch % CPR) * 8 >= Nk) vreg[it] = u32x4{0u, 0u, 0u, 0u};
+            }
+        }
 #pragma unroll
-        for (int it = 0; it < VCH; ++it) *(u32x4*)(buf + KBYTES + vso[it]) = vreg[it];
+        for (int it = 0; it < KCH; ++it) *(u32x4*)((kact ? buf : smem) + kso[it]) = kreg[it];
+#pragma unroll
+        for (int it = 0; it < VCH; ++it) *(u32x4*)((vact ? buf : smem) + KBYTES + vso[it]) = vreg[it];
     };
 
     auto compute = [&](const char* klds, const char* vlds, int j) {
-        f32x16 sacc[2];
+        f32x16 sacc[NQB][NKB];
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+        for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
-            for (int x = 0; x < 16; ++x) sacc[kb][x] = 0.0f;
+            for (int u = 0; u < NQB; ++u)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) sacc[u][kb][x] = 0.0f;
 #pragma unroll
             for (int s = 0; s < D / 16; ++s) {
                 const char* a = klds + koff[kb] + 16 * s * KROW;
                 const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
                 const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW));
                 const F8 af = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                sacc[kb] = mfma32x32x16(af, qf[s], sacc[kb]);
+#pragma unroll
+                for (int u = 0; u < NQB; ++u) sacc[u][kb] = mfma32x32x16(af, qf[u][s], sacc[u][kb]);
             }
         }
-        const int key0 = j * kBN;
-        if (key0 + kBN > Nk) {
+        if (ragged && j == NT - 1) {
+            const int key0 = j * BN;
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+            for (int u = 0; u < NQB; ++u)
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) {
+                        const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+                        if (key0 + kt >= Nk) sacc[u][kb][x] = kNegInf;
+                    }
+        }
+        F8 pf[NQB][NKB][2];
+#pragma unroll
+        for (int u = 0; u < NQB; ++u) {
+            float pm[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sacc[u][kb][x]);
+            const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+            m_true[u] = fmaxf(m_true[u], mt);
+            if (__builtin_amdgcn_ballot_w64(mt > m_used[u] + thr_raw) != 0) {
+                const float m_new = fmaxf(m_used[u], mt);
+                const float alpha = exp2_fast((m_used[u] - m_new) * c);
+                l_run[u] *= alpha;
+#pragma unroll
+                for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) oacc[u][cb][x] *= alpha;
+                m_used[u] = m_new;
+            }
+            const float mc = m_used[u] * c;
+            float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
                 for (int x = 0; x < 16; ++x) {
-                    const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
-                    if (key0 + kt >= Nk) sacc[kb][x] = kNegInf;
+                    const float pv = exp2_fast(fmaf(sacc[u][kb][x], c, -mc));
+                    ps[x & 3] += pv;
+                    pf[u][kb][x >> 3][x & 7] = (T)pv;
                 }
+            l_run[u] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
         }
-        float mt = kNegInf;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) mt = fmaxf(mt, sacc[kb][x]);
-        mt = swap_halves_max(mt);
-        m_true = fmaxf(m_true, mt);
-        if (__builtin_amdgcn_ballot_w64(mt > m_used + thr_raw) != 0) {   // wave-uniform, rare
-            const float m_new = fmaxf(m_used, mt);
-            const float alpha = exp2_fast((m_used - m_new) * c);
-            l_run *= alpha;
-#pragma unroll
-            for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) oacc[cb][x] *= alpha;
-            m_used = m_new;
-        }
-        const float mc = m_used * c;
-        float ls = 0.0f;
-        F8 pf[2][2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const float pv = exp2_fast(fmaf(sacc[kb][x], c, -mc));
-                ls += pv;
-                pf[kb][x >> 3][x & 7] = (T)pv;
-            }
-        l_run += ls;
 #pragma unroll
         for (int cb = 0; cb < DV / 32; ++cb)
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+            for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     const F8 va = *(const F8*)(vlds + voff + cb * 32 * VROW + (kb * 32 + 16 * s) * 2);
-                    oacc[cb] = mfma32x32x16(va, pf[kb][s], oacc[cb]);
+#pragma unroll
+                    for (int u = 0; u < NQB; ++u) oacc[u][cb] = mfma32x32x16(va, pf[u][kb][s], oacc[u][cb]);
                 }
     };
 
-    const int ntiles = (Nk + kBN - 1) / kBN;
     char* const buf0 = smem;
     char* const buf1 = smem + STAGE;
     gload(0);
-    lstore(buf0);
+    lstore(buf0, 0);
     __syncthreads();
-    for (int j = 0; j < ntiles; j += 2) {
-        gload(min(j + 1, ntiles - 1));
+    for (int j = 0; j < NT; j += 2) {
+        gload(min(j + 1, NT - 1));
         compute(buf0, buf0 + KBYTES, j);
-        lstore(buf1);
+        lstore(buf1, min(j + 1, NT - 1));
         __syncthreads();
-        if (j + 1 < ntiles) {
-            gload(min(j + 2, ntiles - 1));
+        if (j + 1 < NT) {
+            gload(min(j + 2, NT - 1));
             compute(buf1, buf1 + KBYTES, j + 1);
-            lstore(buf0);
+            lstore(buf0, min(j + 2, NT - 1));
             __syncthreads();
         }
     }
 
-    const float lt = swap_halves_sum(l_run);
-    const float inv = 1.0f / lt;
-    if (qi < N) {
-        T* Ob = (T*)p.O + (int64_t)b * N * dv;
 #pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
+    for (int u = 0; u < NQB; ++u) {
+        const int qi = qiv[u];
+        const float lt = swap_halves_sum(l_run[u]);
+        const float inv = 1.0f / lt;
+        if (qi < N) {
+            T* Ob = (T*)p.O + (int64_t)b * N * dv;
 #pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int cc = cb * 32 + acc_row(x, h);
-                if (cc < dv) Ob[(int64_t)cc * N + qi] = (T)(oacc[cb][x] * inv);
+            for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) {
+                    const int cc = cb * 32 + acc_row(x, h);
+                    if (cc < dv) Ob[(int64_t)cc * N + qi] = (T)(oacc[u][cb][x] * inv);
+                }
+            if (h == 0) {
+                p.m[(int64_t)b * N + qi] = m_true[u] * p.scale;
+                p.l[(int64_t)b * N + qi] = lt * exp2_fast((m_used[u] - m_true[u]) * c);
             }
-        if (h == 0) {
-            p.m[(int64_t)b * N + qi] = m_true * p.scale;
-            p.l[(int64_t)b * N + qi] = lt * exp2_fast((m_used - m_true) * c);
         }
     }
 }
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256, 2) void dense_fwd_w4b64(FwdParams p) { dense_fwd_tiled<T, D, DV, 4, 64, 1>(p); }
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void dense_fwd_w8b64(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 1>(p); }
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256, 2) void dense_fwd_w4q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 4, 64, 2>(p); }
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
 
 // --------------------------------------------------------------------------
 // launcher
@@ -650,12 +705,29 @@ __global__ __launch_bounds__(kThreads, 2) void dense_fwd_fast(FwdParams p) {
 template <class T, int D>
 static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
     if (p.fast) {
-        switch (DVc) {
-            case 32: hipLaunchKernelGGL((dense_fwd_fast<T, D, 32>), grid, dim3(kThreads), 0, s, p); break;
-            case 64: hipLaunchKernelGGL((dense_fwd_fast<T, D, 64>), grid, dim3(kThreads), 0, s, p); break;
-            case 128: hipLaunchKernelGGL((dense_fwd_fast<T, D, 128>), grid, dim3(kThreads), 0, s, p); break;
-            default: return hipErrorInvalidValue;
+        // geometry per head-dim class (measured on MI355X):
+        // <= 64: 8 waves x 2 query blocks (512 rows / workgroup); 128: 8 waves x 1.
+        int v = g_fwd_variant;
+        if (v == 0) v = (D <= 64 && DVc <= 64) ? 7 : 5;
+        const int nw = (v == 5 || v == 7) ? 8 : 4;
+        const int nqb = v >= 6 ? 2 : 1;
+        FwdParams q = p;
+        q.nqb = (q.N + 32 * nw * nqb - 1) / (32 * nw * nqb);
+        q.total_wg = q.nqb * (int)(p.total_wg / p.nqb);
+        const dim3 g2((unsigned)q.total_wg);
+        const dim3 blk(64 * nw);
+#define FA_LAUNCH_T(KER)                                                                \
+        switch (DVc) {                                                                  \
+            case 32: hipLaunchKernelGGL((KER<T, D, 32>), g2, blk, 0, s, q); break;      \
+            case 64: hipLaunchKernelGGL((KER<T, D, 64>), g2, blk, 0, s, q); break;      \
+            case 128: hipLaunchKernelGGL((KER<T, D, 128>), g2, blk, 0, s, q); break;    \
+            default: return hipErrorInvalidValue;                                       \
         }
+        if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
+        else if (v == 5) { FA_LAUNCH_T(dense_fwd_w8b64) }
+        else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
+        else { FA_LAUNCH_T(dense_fwd_w8q2) }
+#undef FA_LAUNCH_T
         return hipGetLastError();
     }
     switch (DVc) {

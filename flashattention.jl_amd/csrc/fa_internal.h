@@ -80,4 +80,6 @@ inline int head_dim_class(int64_t d) {
 
 constexpr int kMaxHeadDim = 128;
 
+extern int g_fwd_variant;  // forward kernel variant (debug/benchmark knob)
+
 }  // namespace fa
