@@ -82,6 +82,13 @@ int fa_debug_set_fwd_variant(int v) {
     return old;
 }
 
+// Not part of the public header: 1 forces the generic (SIMT) backward.
+int fa_debug_set_bwd_generic(int v) {
+    const int old = fa::g_bwd_force_generic;
+    fa::g_bwd_force_generic = v != 0;
+    return old;
+}
+
 int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
                  int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch, float scale,
                  void* hip_stream) {

@@ -30,9 +30,10 @@ struct BwdParams {
     const void *Q, *K, *V, *O, *dO;
     const float *l, *m;
     void *dQ, *dK, *dV;
-    float* Dv;     // workspace: rowsum(dO ∘ O)   [batch][N]
-    float* lse2;   // workspace: (m + ln l)·log2e [batch][N]
+    float* nD;     // workspace: −rowsum(dO ∘ O)          [batch][N]
+    float* nlse;   // workspace: −(m + ln l)/τ (raw units) [batch][N]
     int N, Nk, d, dv, batch;
+    int nblk, total_wg;          // fast path: row blocks per slab, workgroups
     float scale, scale_log2;
 };
 
@@ -51,8 +52,8 @@ __global__ __launch_bounds__(256) void bwd_prepass(BwdParams p) {
     const T* dO = (const T*)p.dO + b * (int64_t)p.N * p.dv + n;
     float acc = 0.0f;
     for (int c = 0; c < p.dv; ++c) acc = fmaf(to_f(dO[(int64_t)c * p.N]), to_f(O[(int64_t)c * p.N]), acc);
-    p.Dv[idx] = acc;
-    p.lse2[idx] = (p.m[idx] + logf(p.l[idx])) * kLog2e;
+    p.nD[idx] = -acc;
+    p.nlse[idx] = -(p.m[idx] + logf(p.l[idx])) / p.scale;
 }
 
 // --------------------------------------------------------------------------
@@ -91,8 +92,8 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dq(BwdParams p) {
     float acc[kMaxPer];
 #pragma unroll
     for (int t = 0; t < kMaxPer; ++t) acc[t] = 0.0f;
-    const float* Dv = p.Dv + (int64_t)b * N;
-    const float* L2 = p.lse2 + (int64_t)b * N;
+    const float* nD = p.nD + (int64_t)b * N;
+    const float* nL = p.nlse + (int64_t)b * N;
     for (int k0 = 0; k0 < Nk; k0 += kGT) {
         __syncthreads();
         for (int i = tid; i < kGT * d; i += kGThreads) {
@@ -111,8 +112,8 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dq(BwdParams p) {
                 float s = 0.0f, dp = 0.0f;
                 for (int f = 0; f < d; ++f) s = fmaf(sQ[q * d + f], sK[k * d + f], s);
                 for (int f = 0; f < dv; ++f) dp = fmaf(sdO[q * dv + f], sV[k * dv + f], dp);
-                const float pr = exp2f(s * p.scale_log2 - L2[q0 + q]);
-                ds = pr * (dp - Dv[q0 + q]);
+                const float pr = exp2f((s + nL[q0 + q]) * p.scale_log2);
+                ds = pr * (dp + nD[q0 + q]);
             }
             sdS[q * (kGT + 1) + k] = ds;
         }
@@ -165,8 +166,8 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
     float accK[kMaxPer], accV[kMaxPer];
 #pragma unroll
     for (int t = 0; t < kMaxPer; ++t) { accK[t] = 0.0f; accV[t] = 0.0f; }
-    const float* Dv = p.Dv + (int64_t)b * N;
-    const float* L2 = p.lse2 + (int64_t)b * N;
+    const float* nD = p.nD + (int64_t)b * N;
+    const float* nL = p.nlse + (int64_t)b * N;
     for (int q0 = 0; q0 < N; q0 += kGT) {
         __syncthreads();
         for (int i = tid; i < kGT * d; i += kGThreads) {
@@ -185,8 +186,8 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
                 float s = 0.0f, dp = 0.0f;
                 for (int f = 0; f < d; ++f) s = fmaf(sQ[q * d + f], sK[k * d + f], s);
                 for (int f = 0; f < dv; ++f) dp = fmaf(sdO[q * dv + f], sV[k * dv + f], dp);
-                pr = exp2f(s * p.scale_log2 - L2[q0 + q]);
-                ds = pr * (dp - Dv[q0 + q]);
+                pr = exp2f((s + nL[q0 + q]) * p.scale_log2);
+                ds = pr * (dp + nD[q0 + q]);
             }
             sP[q * (kGT + 1) + k] = pr;
             sdS[q * (kGT + 1) + k] = ds;
@@ -219,6 +220,348 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
     }
 }
 
+
+// --------------------------------------------------------------------------
+// 2./3. MFMA fast path (bf16 / fp16; d, dv in {32, 64, 128}; N, Nk % 8 == 0;
+// 16-B aligned).  Token tiles of 64 are staged by LDS-DMA (buffer_load … lds)
+// into [rows][64 tokens] images with 128-B rows and a 16-B XOR swizzle
+// g(f) = ((f>>3)&3) | ((f>>1)&1)<<2 that makes BOTH access patterns
+// conflict-free: the transposed reads ds_read_b64_tr_b16 (A operands of the
+// score / dP products: 4 consecutive rows × 64 B per half-wave) and the
+// ds_read_b128 row reads (A operands of the gradient products: 16 rows per
+// lane group, one 16-B chunk each).
+// --------------------------------------------------------------------------
+__device__ __forceinline__ int swz16(int f) { return ((f >> 3) & 3) | (((f >> 1) & 1) << 2); }
+
+template <class T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bslab(const void* base, int64_t off_elems, int64_t elems) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const T*)base + off_elems), (short)0,
+                                             (int)(elems * (int64_t)sizeof(T)), 0x00020000);
+}
+
+// LDS-DMA one [R rows][64 tokens] image (R*128 bytes) from a [*][ntok] slab at
+// token t0.  4 waves; each wave-instruction fills 1 KiB (8 rows) lane-linearly,
+// so the swizzle is applied to the per-lane GLOBAL address (cdna guide rule 21).
+template <int R>
+__device__ __forceinline__ void dma_image(__amdgpu_buffer_rsrc_t rs, char* img, int ntok, int t0, int wave, int lane) {
+#pragma unroll
+    for (int it = 0; it < R / 32; ++it) {
+        const int blk = it * 4 + wave;                 // 1-KiB block of the image
+        const int P = blk * 64 + lane;                 // 16-B chunk index (linear in LDS)
+        const int f = P >> 3, c = (P & 7) ^ swz16(f);  // logical chunk at that position
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16,
+            (f * ntok + t0 + 8 * c) * 2, 0, 0, 0);
+    }
+}
+
+// Per-lane constant parts of the two fragment reads of an image.
+struct FragAddr {
+    int tr[2][2];   // [token block tb][s & 1] byte offset of the transposed read (half2 = 0)
+    int row[2];     // [h-independent] b128 row read: swizzled chunk offsets need (r, chunk)
+};
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256, 2) void bwd_dq_fast(BwdParams p) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int KB = D * 128, VB = DV * 128, STAGE = KB + VB;
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int lid = xcd_remap(blockIdx.x, p.total_wg);
+    const int b = lid / p.nblk, qb = lid - b * p.nblk;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int N = p.N, Nk = p.Nk;
+    const auto qrs = bslab<T>(p.Q, (int64_t)b * N * D, (int64_t)N * D);
+    const auto ors = bslab<T>(p.dO, (int64_t)b * N * DV, (int64_t)N * DV);
+    const auto krs = bslab<T>(p.K, (int64_t)b * Nk * D, (int64_t)Nk * D);
+    const auto vrs = bslab<T>(p.V, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
+    const int qi = qb * 128 + wave * 32 + r;
+    F8 qf[D / 16], df[DV / 16];
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            qf[s][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(qrs, ((16 * s + 8 * h + e) * N + qi) * 2, 0, 0));
+#pragma unroll
+    for (int s = 0; s < DV / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            df[s][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(ors, ((16 * s + 8 * h + e) * N + qi) * 2, 0, 0));
+    const int qc = qi < N ? qi : N - 1;
+    const float c = p.scale_log2;
+    const float cnl = c * p.nlse[(int64_t)b * N + qc];
+    const float nDq = p.nD[(int64_t)b * N + qc];
+
+    // transposed-read lane offsets (see fa_fwd.hip): lane 4q+pp of 16-lane group g
+    const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    int tro[2][2];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+            const int sw = ((sp << 1) | h) | (((qq >> 1) & 1) << 2);
+            tro[tb][sp] = (8 * h + qq) * 128 + (((tb * 4 + kh * 2 + (sig >> 1)) ^ sw) * 16) + (sig & 1) * 8;
+        }
+    const int rsw = swz16(r);
+    auto trfrag = [&](const char* img, int tb, int s) -> F8 {
+        const char* a = img + tro[tb][s & 1] + 16 * s * 128;
+        const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+        const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto rowfrag = [&](const char* img, int cb, int tb, int s2) -> F8 {
+        return *(const F8*)(img + (cb * 32 + r) * 128 + (((tb * 4 + 2 * s2 + h) ^ rsw) * 16));
+    };
+
+    f32x16 dq[D / 32];
+#pragma unroll
+    for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) dq[cb][x] = 0.0f;
+
+    auto fill = [&](char* st, int t) {
+        dma_image<D>(krs, st, Nk, t * 64, wave, lane);
+        dma_image<DV>(vrs, st + KB, Nk, t * 64, wave, lane);
+    };
+    auto compute = [&](const char* st, int t) {
+        const char* kimg = st;
+        const char* vimg = st + KB;
+        const bool partial = (t + 1) * 64 > Nk;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 sa, dp;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) { sa[x] = 0.0f; dp[x] = 0.0f; }
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) sa = mfma32x32x16(trfrag(kimg, kb, s), qf[s], sa);
+#pragma unroll
+            for (int s = 0; s < DV / 16; ++s) dp = mfma32x32x16(trfrag(vimg, kb, s), df[s], dp);
+            if (partial) {
+#pragma unroll
+                for (int x = 0; x < 16; ++x)
+                    if (t * 64 + kb * 32 + (x & 7) + 8 * h + 16 * (x >> 3) >= Nk) sa[x] = kNegInf;
+            }
+            F8 dsf[2];
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = exp2_fast(fmaf(sa[x], c, cnl));
+                dsf[x >> 3][x & 7] = (T)(pr * (dp[x] + nDq));
+            }
+#pragma unroll
+            for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) dq[cb] = mfma32x32x16(rowfrag(kimg, cb, kb, s2), dsf[s2], dq[cb]);
+        }
+    };
+
+    const int NT = (Nk + 63) / 64;
+    char* const st0 = smem;
+    char* const st1 = smem + STAGE;
+    fill(st0, 0);
+    __syncthreads();
+    for (int t = 0; t < NT; t += 2) {
+        fill(st1, min(t + 1, NT - 1));
+        compute(st0, t);
+        __syncthreads();
+        if (t + 1 < NT) {
+            fill(st0, min(t + 2, NT - 1));
+            compute(st1, t + 1);
+            __syncthreads();
+        }
+    }
+    if (qi < N) {
+        T* dQb = (T*)p.dQ + (int64_t)b * N * D;
+#pragma unroll
+        for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                dQb[(int64_t)(cb * 32 + acc_row(x, h)) * N + qi] = (T)(dq[cb][x] * p.scale);
+    }
+}
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int QB = D * 128, OB = DV * 128, STAGE = QB + OB + 512;
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int lid = xcd_remap(blockIdx.x, p.total_wg);
+    const int b = lid / p.nblk, kblk = lid - b * p.nblk;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int N = p.N, Nk = p.Nk;
+    const auto qrs = bslab<T>(p.Q, (int64_t)b * N * D, (int64_t)N * D);
+    const auto ors = bslab<T>(p.dO, (int64_t)b * N * DV, (int64_t)N * DV);
+    const auto krs = bslab<T>(p.K, (int64_t)b * Nk * D, (int64_t)Nk * D);
+    const auto vrs = bslab<T>(p.V, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
+    const int kj = kblk * 128 + wave * 32 + r;   // this lane's key (column of S, dP)
+    F8 kf[D / 16], vf[DV / 16];
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            kf[s][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(krs, ((16 * s + 8 * h + e) * Nk + kj) * 2, 0, 0));
+#pragma unroll
+    for (int s = 0; s < DV / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            vf[s][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(vrs, ((16 * s + 8 * h + e) * Nk + kj) * 2, 0, 0));
+    const float c = p.scale_log2;
+    const float* nlse = p.nlse + (int64_t)b * N;
+    const float* nDg = p.nD + (int64_t)b * N;
+
+    const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    int tro[2][2];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+            const int sw = ((sp << 1) | h) | (((qq >> 1) & 1) << 2);
+            tro[tb][sp] = (8 * h + qq) * 128 + (((tb * 4 + kh * 2 + (sig >> 1)) ^ sw) * 16) + (sig & 1) * 8;
+        }
+    const int rsw = swz16(r);
+    auto trfrag = [&](const char* img, int tb, int s) -> F8 {
+        const char* a = img + tro[tb][s & 1] + 16 * s * 128;
+        const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+        const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto rowfrag = [&](const char* img, int cb, int tb, int s2) -> F8 {
+        return *(const F8*)(img + (cb * 32 + r) * 128 + (((tb * 4 + 2 * s2 + h) ^ rsw) * 16));
+    };
+
+    f32x16 dk[D / 32], dv[DV / 32];
+#pragma unroll
+    for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) dk[cb][x] = 0.0f;
+#pragma unroll
+    for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) dv[cb][x] = 0.0f;
+
+    // per-tile row constants: threads 0-63 carry −lse (−inf past N), 64-127 −D
+    float rowc = 0.0f;
+    auto load_rowc = [&](int t) {
+        const int q = t * 64 + (tid & 63);
+        if (tid < 64) rowc = q < N ? nlse[q] : kNegInf;
+        else if (tid < 128) rowc = q < N ? nDg[q] : 0.0f;
+    };
+    auto store_rowc = [&](char* st) {
+        if (tid < 128) ((float*)(st + QB + OB))[tid] = rowc;
+    };
+    auto fill = [&](char* st, int t) {
+        dma_image<D>(qrs, st, N, t * 64, wave, lane);
+        dma_image<DV>(ors, st + QB, N, t * 64, wave, lane);
+    };
+    auto compute = [&](const char* st) {
+        const char* qimg = st;
+        const char* oimg = st + QB;
+        const float* rl = (const float*)(st + QB + OB);      // −lse[64], then −D[64]
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            // rows of S / dP (queries) map to 8h + {0..7} and 16 + 8h + {0..7}
+            f32x16 sa, dp;
+            const f32x4* Lq = (const f32x4*)(rl + u * 32 + 8 * h);
+            const f32x4* Dq = (const f32x4*)(rl + 64 + u * 32 + 8 * h);
+            const f32x4 l0 = Lq[0], l1 = Lq[1], l2 = Lq[4], l3 = Lq[5];
+            const f32x4 d0 = Dq[0], d1 = Dq[1], d2 = Dq[4], d3 = Dq[5];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sa[e] = l0[e]; sa[4 + e] = l1[e]; sa[8 + e] = l2[e]; sa[12 + e] = l3[e];
+                dp[e] = d0[e]; dp[4 + e] = d1[e]; dp[8 + e] = d2[e]; dp[12 + e] = d3[e];
+            }
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) sa = mfma32x32x16(trfrag(qimg, u, s), kf[s], sa);
+#pragma unroll
+            for (int s = 0; s < DV / 16; ++s) dp = mfma32x32x16(trfrag(oimg, u, s), vf[s], dp);
+            F8 pf[2], dsf[2];
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = exp2_fast(sa[x] * c);
+                pf[x >> 3][x & 7] = (T)pr;
+                dsf[x >> 3][x & 7] = (T)(pr * dp[x]);
+            }
+#pragma unroll
+            for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) dv[cb] = mfma32x32x16(rowfrag(oimg, cb, u, s2), pf[s2], dv[cb]);
+#pragma unroll
+            for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) dk[cb] = mfma32x32x16(rowfrag(qimg, cb, u, s2), dsf[s2], dk[cb]);
+        }
+    };
+
+    const int NT = (N + 63) / 64;
+    char* const st0 = smem;
+    char* const st1 = smem + STAGE;
+    load_rowc(0);
+    fill(st0, 0);
+    store_rowc(st0);
+    __syncthreads();
+    for (int t = 0; t < NT; t += 2) {
+        load_rowc(min(t + 1, NT - 1));
+        fill(st1, min(t + 1, NT - 1));
+        compute(st0);
+        store_rowc(st1);
+        __syncthreads();
+        if (t + 1 < NT) {
+            load_rowc(min(t + 2, NT - 1));
+            fill(st0, min(t + 2, NT - 1));
+            compute(st1);
+            store_rowc(st0);
+            __syncthreads();
+        }
+    }
+    if (kj < Nk) {
+        T* dKb = (T*)p.dK + (int64_t)b * Nk * D;
+        T* dVb = (T*)p.dV + (int64_t)b * Nk * DV;
+#pragma unroll
+        for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                dKb[(int64_t)(cb * 32 + acc_row(x, h)) * Nk + kj] = (T)(dk[cb][x] * p.scale);
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                dVb[(int64_t)(cb * 32 + acc_row(x, h)) * Nk + kj] = (T)dv[cb][x];
+    }
+}
+
+int g_bwd_force_generic = 0;   // benchmark knob
+
+template <class T, int D, int DV>
+static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
+    p.nblk = (p.N + 127) / 128;
+    p.total_wg = p.nblk * p.batch;
+    hipLaunchKernelGGL((bwd_dq_fast<T, D, DV>), dim3((unsigned)p.total_wg), dim3(256), 0, s, p);
+    p.nblk = (p.Nk + 127) / 128;
+    p.total_wg = p.nblk * p.batch;
+    hipLaunchKernelGGL((bwd_dkdv_fast<T, D, DV>), dim3((unsigned)p.total_wg), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+template <class T, int D>
+static hipError_t launch_fast_d(const BwdParams& p, hipStream_t s) {
+    switch (p.dv) {
+        case 32: return launch_fast_dd<T, D, 32>(p, s);
+        case 64: return launch_fast_dd<T, D, 64>(p, s);
+        case 128: return launch_fast_dd<T, D, 128>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
+template <class T>
+static hipError_t launch_fast(const BwdParams& p, hipStream_t s) {
+    switch (p.d) {
+        case 32: return launch_fast_d<T, 32>(p, s);
+        case 64: return launch_fast_d<T, 64>(p, s);
+        case 128: return launch_fast_d<T, 128>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 // --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
@@ -241,13 +584,18 @@ static hipError_t launch_generic(const BwdParams& p, hipStream_t s) {
 }
 
 template <class T>
-static hipError_t launch_typed(const BwdParams& p, hipStream_t s) {
+static hipError_t launch_typed(const BwdParams& p, hipStream_t s, bool fast) {
     const int64_t total = (int64_t)p.N * p.batch;
     hipLaunchKernelGGL(bwd_prepass<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if constexpr (!std::is_same<T, float>::value) {
+        if (fast) return launch_fast<T>(p, s);
+    }
     return launch_generic<T>(p, s);
 }
+
+static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
 int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
@@ -263,16 +611,21 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     p.Q = a.Q; p.K = a.K; p.V = a.V; p.O = a.O; p.dO = a.dO; p.l = a.l; p.m = a.m;
     p.dQ = a.dQ; p.dK = a.dK; p.dV = a.dV;
     const uintptr_t ws = ((uintptr_t)a.workspace + 255) & ~(uintptr_t)255;
-    p.Dv = (float*)ws;
-    p.lse2 = p.Dv + a.N * a.batch;
+    p.nD = (float*)ws;
+    p.nlse = p.nD + a.N * a.batch;
     p.N = (int)a.N; p.Nk = (int)a.Nk; p.d = (int)a.d; p.dv = (int)a.dv; p.batch = (int)a.batch;
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
+    auto cls = [](int64_t x) { return x == 32 || x == 64 || x == 128; };
+    const bool fast = !g_bwd_force_generic && a.dtype != FA_DTYPE_F32 && cls(a.d) && cls(a.dv) &&
+                      a.N % 8 == 0 && a.Nk % 8 == 0 && a.N * a.d * 2 < INT32_MAX &&
+                      a.Nk * a.d * 2 < INT32_MAX && a.N * a.dv * 2 < INT32_MAX && a.Nk * a.dv * 2 < INT32_MAX &&
+                      aligned16(a.Q) && aligned16(a.K) && aligned16(a.V) && aligned16(a.dO);
     hipError_t e;
     switch (a.dtype) {
-        case FA_DTYPE_BF16: e = launch_typed<bf16>(p, s); break;
-        case FA_DTYPE_F16: e = launch_typed<f16>(p, s); break;
-        case FA_DTYPE_F32: e = launch_typed<float>(p, s); break;
+        case FA_DTYPE_BF16: e = launch_typed<bf16>(p, s, fast); break;
+        case FA_DTYPE_F16: e = launch_typed<f16>(p, s, fast); break;
+        case FA_DTYPE_F32: e = launch_typed<float>(p, s, false); break;
         default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
     }
     if (e != hipSuccess) {

@@ -80,6 +80,7 @@ inline int head_dim_class(int64_t d) {
 
 constexpr int kMaxHeadDim = 128;
 
-extern int g_fwd_variant;  // forward kernel variant (debug/benchmark knob)
+extern int g_fwd_variant;       // forward kernel variant (debug/benchmark knob)
+extern int g_bwd_force_generic; // backward: force the generic SIMT path (debug knob)
 
 }  // namespace fa

@@ -108,6 +108,10 @@ def lib() -> ctypes.CDLL:
                                   ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64,
                                   f32, vp, ctypes.c_size_t, vp]
     del fp
+    for dbg in ("fa_debug_set_fwd_variant", "fa_debug_set_bwd_generic"):
+        if hasattr(L, dbg):
+            getattr(L, dbg).restype = ctypes.c_int
+            getattr(L, dbg).argtypes = [ctypes.c_int]
     if L.fa_abi_version() != 1:
         raise ImportError("fa_hip: ABI version mismatch")
     _LIB = L

@@ -67,8 +67,10 @@ def test_backward_golden(fa, path, dtype):
 
 @pytest.mark.parametrize("N,Nk,d,dv,B", [(64, 64, 64, 64, 2), (256, 192, 128, 128, 2), (100, 77, 12, 6, 3),
                                          (512, 512, 64, 64, 4), (1, 5, 16, 16, 1), (130, 1, 32, 8, 2),
-                                         (1024, 1024, 128, 128, 1), (200, 320, 64, 128, 2)])
-@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+                                         (1024, 1024, 128, 128, 1), (200, 320, 64, 128, 2),
+                                         (264, 136, 128, 64, 2), (8, 8, 32, 32, 3), (72, 1000, 128, 32, 1),
+                                         (1000, 8, 64, 64, 1)])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
 def test_backward_vs_oracle_random(fa, N, Nk, d, dv, B, dtype):
     rng = np.random.default_rng(N * 31 + Nk)
     bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
@@ -115,3 +117,22 @@ def test_backward_config4_properties(fa):
     assert float(colsum.abs().max()) <= 2e-2 * float(dK.float().abs().sum(0).max())
     # Σ_keys dV = Σ_q dO (rows of P sum to one)
     assert torch.allclose(dV.float().sum(0), dO.float().sum(0), rtol=2e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("N,Nk,d,dv", [(256, 256, 64, 64), (200, 136, 128, 128)])
+def test_backward_fast_matches_generic(fa, N, Nk, d, dv):
+    """The MFMA fast path and the generic SIMT path agree (same math, same inputs)."""
+    rng = np.random.default_rng(N + d)
+    Q, K, V, dO = (fa.jl_tensor(rng.standard_normal(sh), torch.bfloat16)
+                   for sh in ((N, d, 2), (Nk, d, 2), (Nk, dv, 2), (N, dv, 2)))
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    L = fa.lib()
+    fast = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
+    L.fa_debug_set_bwd_generic(1)
+    try:
+        gen = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
+    finally:
+        L.fa_debug_set_bwd_generic(0)
+    torch.cuda.synchronize()
+    for a, b, nm in zip(fast, gen, ("dQ", "dK", "dV")):
+        assert_grad_close(_np(a), _np(b), "bfloat16", nm)
