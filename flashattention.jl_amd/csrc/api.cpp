@@ -137,9 +137,19 @@ size_t fa_windowed_workspace(int dtype, int nspatial, const int64_t* spatial, in
     return fa::windowed_workspace(dtype, g, d, dv, batch);
 }
 
+size_t fa_windowed_fwd_workspace(int dtype, int nspatial, const int64_t* spatial, int64_t d, int64_t dv,
+                                 int64_t batch, int64_t ws, int64_t stride, int64_t pad) {
+    fa::WindowGeom g;
+    const char* why = "";
+    if (!valid_dtype(dtype) || d < 1 || dv < 1 || batch < 1) return 0;
+    if (make_geom(g, nspatial, spatial, ws, stride, pad, &why) != FA_OK) return 0;
+    return fa::windowed_fwd_workspace(dtype, g, d, dv, batch);
+}
+
 int fa_windowed_fwd(int dtype, const void* q, const void* k, const void* v, void* y, float* l, float* m,
                     int nspatial, const int64_t* spatial, int64_t d, int64_t dv, int64_t batch,
-                    int64_t ws, int64_t stride, int64_t pad, float scale, void* hip_stream) {
+                    int64_t ws, int64_t stride, int64_t pad, float scale, void* workspace,
+                    size_t workspace_bytes, void* hip_stream) {
     static const char* fn = "fa_windowed_fwd";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
     if (d < 1 || dv < 1 || batch < 1)
@@ -152,8 +162,11 @@ int fa_windowed_fwd(int dtype, const void* q, const void* k, const void* v, void
     a.dtype = dtype; a.q = q; a.k = k; a.v = v; a.y = y; a.l = l; a.m = m;
     a.d = d; a.dv = dv; a.batch = batch;
     a.scale = resolve_scale(scale, d);
-    a.workspace = nullptr;
-    a.workspace_bytes = 0;
+    const size_t need = fa::windowed_fwd_workspace(dtype, a.g, d, dv, batch);
+    if (need > 0 && (!workspace || workspace_bytes < need))
+        return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_windowed_fwd_workspace()");
+    a.workspace = workspace;
+    a.workspace_bytes = workspace_bytes;
     rc = fa::launch_windowed_fwd(a, (hipStream_t)hip_stream, &why);
     return rc == FA_OK ? ok() : fail(rc, fn, why);
 }

@@ -67,6 +67,7 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why);
 size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
+size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why);
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why);
 

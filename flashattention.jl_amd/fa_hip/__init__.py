@@ -100,9 +100,13 @@ def lib() -> ctypes.CDLL:
     L.fa_windowed_workspace.restype = ctypes.c_size_t
     L.fa_windowed_workspace.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64),
                                         i64, i64, i64, i64, i64, i64]
+    L.fa_windowed_fwd_workspace.restype = ctypes.c_size_t
+    L.fa_windowed_fwd_workspace.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64),
+                                            i64, i64, i64, i64, i64, i64]
     L.fa_windowed_fwd.restype = ctypes.c_int
     L.fa_windowed_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, ctypes.c_int,
-                                  ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64, f32, vp]
+                                  ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64, f32, vp,
+                                  ctypes.c_size_t, vp]
     L.fa_windowed_bwd.restype = ctypes.c_int
     L.fa_windowed_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                   ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64,
@@ -269,7 +273,7 @@ def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
     dV = jl_empty((Nk, dv, B), Q.dtype, Q.device)
     L = lib()
     nws = L.fa_dense_bwd_workspace(code, N, Nk, d, dv, B)
-    ws = torch.empty(max(int(nws), 1), dtype=torch.uint8, device=Q.device)
+    ws = _workspace(Q.device, nws)
     _check(L.fa_dense_bwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(dO), _ptr(l), _ptr(m),
                           _ptr(dQ), _ptr(dK), _ptr(dV), N, Nk, d, dv, B, float(scale),
                           _ptr(ws), int(nws), _stream(Q)))
@@ -284,6 +288,21 @@ def window_geometry(spatial: Sequence[int], ws: int, stride: int, pad: int):
     out = tuple((s + 2 * pad - ws) // stride + 1 for s in spatial)
     _require(all(o >= 1 for o in out), "window larger than the padded input")
     return out
+
+
+_WS = {}
+
+
+def _workspace(device, nbytes: int) -> torch.Tensor:
+    """Scratch buffer for the C ABI's workspace arguments (cached per device,
+    grown on demand; reuse is safe because all calls run on the caller's stream
+    in order)."""
+    key = (device.type, device.index)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < max(int(nbytes), 1):
+        buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
 
 
 def _i64_array(xs):
@@ -318,9 +337,13 @@ def windowed_fa(q, k, v, windowsize: int, stride: Optional[int] = None,
     y = jl_empty(sp + (dv, B), q.dtype, q.device)
     lw = jl_empty((T, 1, L, B), torch.float32, q.device)
     mw = jl_empty((T, 1, L, B), torch.float32, q.device)
-    _check(lib().fa_windowed_fwd(code, _ptr(q), _ptr(k), _ptr(v), _ptr(y), _ptr(lw), _ptr(mw),
-                                 nsp, _i64_array(sp), d, dv, B, windowsize, stride, pad,
-                                 float(scale), _stream(q)))
+    Lb = lib()
+    spa = _i64_array(sp)
+    nws = Lb.fa_windowed_fwd_workspace(code, nsp, spa, d, dv, B, windowsize, stride, pad)
+    ws = _workspace(q.device, nws)
+    _check(Lb.fa_windowed_fwd(code, _ptr(q), _ptr(k), _ptr(v), _ptr(y), _ptr(lw), _ptr(mw),
+                              nsp, spa, d, dv, B, windowsize, stride, pad,
+                              float(scale), _ptr(ws), int(nws), _stream(q)))
     return y, lw, mw
 
 
@@ -347,7 +370,7 @@ def windowed_fa_backward(q, k, v, y, dy, l, m, windowsize: int, stride: Optional
     Lb = lib()
     spa = _i64_array(sp)
     nws = Lb.fa_windowed_workspace(code, nsp, spa, d, dv, B, windowsize, stride, pad)
-    ws = torch.empty(max(int(nws), 1), dtype=torch.uint8, device=q.device)
+    ws = _workspace(q.device, nws)
     _check(Lb.fa_windowed_bwd(code, _ptr(q), _ptr(k), _ptr(v), _ptr(y), _ptr(dy), _ptr(l), _ptr(m),
                               _ptr(dq), _ptr(dk), _ptr(dvv), nsp, spa, d, dv, B, windowsize,
                               stride, pad, float(scale), _ptr(ws), int(nws), _stream(q)))

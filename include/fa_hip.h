@@ -100,9 +100,17 @@ int fa_windowed_fwd(int dtype,
                     int nspatial, const int64_t* spatial,
                     int64_t d, int64_t dv, int64_t batch,
                     int64_t ws, int64_t stride, int64_t pad,
-                    float scale, void* hip_stream);
+                    float scale, void* workspace, size_t workspace_bytes,
+                    void* hip_stream);
 
-/* Workspace for fa_windowed_fwd / fa_windowed_bwd (bytes; 0 is valid). */
+/* Workspace bytes fa_windowed_fwd needs (0 is a valid answer: the fused
+ * single-pass kernel needs none; large windows / fp32 use a composed
+ * gather -> dense -> fold path that stages windows in the workspace). */
+size_t fa_windowed_fwd_workspace(int dtype, int nspatial, const int64_t* spatial,
+                                 int64_t d, int64_t dv, int64_t batch,
+                                 int64_t ws, int64_t stride, int64_t pad);
+
+/* Workspace bytes fa_windowed_bwd needs. */
 size_t fa_windowed_workspace(int dtype, int nspatial, const int64_t* spatial,
                              int64_t d, int64_t dv, int64_t batch,
                              int64_t ws, int64_t stride, int64_t pad);

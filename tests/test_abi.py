@@ -26,8 +26,8 @@ def declared_functions():
 def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("fa_dense_fwd", "fa_dense_bwd", "fa_dense_bwd_workspace", "fa_windowed_fwd",
-              "fa_windowed_bwd", "fa_windowed_workspace", "fa_last_error", "fa_abi_version",
-              "fa_max_head_dim"):
+              "fa_windowed_fwd_workspace", "fa_windowed_bwd", "fa_windowed_workspace",
+              "fa_last_error", "fa_abi_version", "fa_max_head_dim"):
         assert f in fns
 
 
@@ -72,9 +72,9 @@ def test_invalid_arguments_return_status_and_message():
     assert rc == fa_hip.FA_ERR_UNSUPPORTED and b"head dimension" in L.fa_last_error()
     # windowed: window larger than padded input
     sp = (ctypes.c_int64 * 2)(5, 5)
-    rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 2, sp, 4, 4, 1, 9, 9, 0, 0.0, None)
+    rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 2, sp, 4, 4, 1, 9, 9, 0, 0.0, None, 0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"window" in L.fa_last_error()
-    rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 4, sp, 4, 4, 1, 3, 3, 0, 0.0, None)
+    rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 4, sp, 4, 4, 1, 3, 3, 0, 0.0, None, 0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"nspatial" in L.fa_last_error()
     # backward: workspace check happens before any launch
     need = L.fa_dense_bwd_workspace(1, 128, 128, 64, 64, 2)
@@ -127,3 +127,15 @@ def test_julia_layout_helpers():
     assert not fa_hip.is_jl_contiguous(torch.empty(5, 3, 2))
     x = torch.arange(30.0).reshape(5, 3, 2)
     assert torch.equal(fa_hip.jl_tensor(x, device="cpu"), x)
+
+
+def test_workspace_queries_are_positive_and_monotone():
+    import fa_hip
+    L = fa_hip.lib()
+    sp = (ctypes.c_int64 * 2)(128, 128)
+    a = L.fa_windowed_workspace(1, 2, sp, 64, 64, 1, 7, 7, 3)
+    b = L.fa_windowed_workspace(1, 2, sp, 64, 64, 4, 7, 7, 3)
+    assert 0 < a < b
+    assert L.fa_windowed_fwd_workspace(1, 2, sp, 64, 64, 1, 7, 7, 3) <= a
+    assert L.fa_dense_bwd_workspace(1, 4096, 4096, 64, 64, 64) >= 2 * 4 * 4096 * 64
+    assert L.fa_dense_bwd_workspace(9, 4096, 4096, 64, 64, 64) == 0   # bad dtype
