@@ -1,0 +1,108 @@
+# FlashAttentionHIP.jl — ccall binding of libfa_hip.so (MI355X / gfx950) for
+# nikopj/FlashAttention.jl.
+#
+# Include from src/FlashAttention.jl next to the disabled CUDA include
+# (reference src/FlashAttention.jl:29):
+#
+#     using AMDGPU
+#     include("hip/FlashAttentionHIP.jl")
+#
+# It adds methods for AMDGPU device arrays (ROCArray) to the reference's own
+# generic functions, exactly like the CUDA precedent
+# `dense_fa!(O::CuArray{T,3}, …)` (src/cuda/flash.jl:121-140), so user code
+# calling dense_fa / dense_fa! / windowed_fa / block_fa on ROCArrays runs on
+# the HIP kernels with no other change.  Arrays keep Julia's column-major
+# layout; the C ABI (include/fa_hip.h) consumes it as is — no copies.
+#
+# NOT EXECUTED in this repository's CI (no Julia in the image); the Python
+# ctypes mirror (flashattention.jl_amd/fa_hip) binds the same symbols and
+# carries the parity tests.
+
+const libfa_hip = get(ENV, "FA_HIP_LIB", joinpath(@__DIR__, "..", "libfa_hip.so"))
+
+const FA_DTYPE = Dict(Float32 => Cint(0), AMDGPU.BFloat16 => Cint(1), Float16 => Cint(2))
+
+fa_dtype(::Type{T}) where {T} = haskey(FA_DTYPE, T) ? FA_DTYPE[T] :
+    throw(ArgumentError("FlashAttentionHIP: element type $T not supported (Float32, Float16, BFloat16)"))
+
+function fa_check(rc::Cint)
+    rc == 0 && return nothing
+    msg = unsafe_string(ccall((:fa_last_error, libfa_hip), Cstring, ()))
+    rc == 1 && occursin("DimensionMismatch", msg) && throw(DimensionMismatch(msg))
+    error("libfa_hip: ", msg)
+end
+
+stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
+
+# dense_fa!(O, l, m, Q, K, V) — replaces the body of src/dense.jl:21-102
+function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T}
+    N, d, B = size(Q)
+    Nk, dv = size(K, 1), size(V, 2)
+    size(K) == (Nk, d, B) || throw(DimensionMismatch("K"))
+    size(V) == (Nk, dv, B) || throw(DimensionMismatch("V"))
+    size(O) == (N, dv, B) || throw(DimensionMismatch("O"))
+    fa_check(ccall((:fa_dense_fwd, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                    Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
+                   fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, stream_ptr()))
+    return O, l, m
+end
+
+# dense_fa(q, k, v) — src/dense.jl:1-19 (l, m are Float32 on the device: DESIGN.md)
+function dense_fa(q::ROCArray{T,D}, k::ROCArray{T,D}, v::ROCArray{T,D}) where {T,D}
+    d, dv, B = size(q, D - 1), size(v, D - 1), size(q, D)
+    Q, K, V = reshape(q, :, d, B), reshape(k, :, d, B), reshape(v, :, dv, B)
+    N = size(Q, 1)
+    O = similar(Q, N, dv, B)                      # dv, not d (reference bug A.1 not inherited)
+    l = similar(Q, Float32, N, 1, B)
+    m = similar(Q, Float32, N, 1, B)
+    dense_fa!(O, l, m, Q, K, V)
+    return reshape(O, size(q)[1:D-2]..., dv, :), l, m
+end
+
+# dense_fa_backward(Q, K, V, O, dO, l, m) — src/dense.jl:104-167
+function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
+                           O::ROCArray{T,3}, dO::ROCArray{T,3},
+                           l::ROCArray{Float32,3}, m::ROCArray{Float32,3}) where {T}
+    N, d, B = size(Q)
+    Nk, dv = size(K, 1), size(V, 2)
+    dQ, dK, dV = similar(Q), similar(K), similar(V)
+    nws = ccall((:fa_dense_bwd_workspace, libfa_hip), Csize_t,
+                (Cint, Int64, Int64, Int64, Int64, Int64), fa_dtype(T), N, Nk, d, dv, B)
+    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    fa_check(ccall((:fa_dense_bwd, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32},
+                    Ptr{Float32}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
+                    Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                   fa_dtype(T), Q, K, V, O, dO, l, m, dQ, dK, dV, N, Nk, d, dv, B, 0f0,
+                   ws, nws, stream_ptr()))
+    return dQ, dK, dV
+end
+
+# windowed_fa(q, k, v, ws; stride, pad) — src/windowed.jl:3-23 (fused on the device)
+function windowed_fa(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,N}, windowsize;
+                     stride=windowsize, pad=(windowsize - 1) ÷ 2) where {T,N}
+    nsp = N - 2
+    spatial = Int64[size(q, i) for i in 1:nsp]
+    d, dv, B = size(q, N - 1), size(v, N - 1), size(q, N)
+    L = prod((s + 2pad - windowsize) ÷ stride + 1 for s in spatial)
+    y = similar(v, size(q)[1:N-2]..., dv, B)
+    l = similar(q, Float32, windowsize^nsp, 1, L, B)
+    m = similar(q, Float32, windowsize^nsp, 1, L, B)
+    nws = ccall((:fa_windowed_fwd_workspace, libfa_hip), Csize_t,
+                (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),
+                fa_dtype(T), nsp, spatial, d, dv, B, windowsize, stride, pad)
+    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    fa_check(ccall((:fa_windowed_fwd, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                    Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64, Cfloat,
+                    Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                   fa_dtype(T), q, k, v, y, l, m, nsp, spatial, d, dv, B, windowsize, stride, pad,
+                   0f0, ws, nws, stream_ptr()))
+    return y, l, m
+end
+
+# block_fa — src/windowed.jl:1
+block_fa(q::ROCArray, k::ROCArray, v::ROCArray, windowsize; pad=0) =
+    windowed_fa(q, k, v, windowsize; stride=windowsize, pad=pad)

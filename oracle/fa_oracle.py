@@ -11,17 +11,21 @@ the reference file:line it follows.  Arrays use the reference's Julia shapes
 (``(spatial..., d, batch)``; the memory order of the numpy array is irrelevant
 here, numpy indexes by shape).
 
-Parity pinning
---------------
-The reference is Julia and cannot run here (no Julia, no NNlib), and it ships
-no golden vectors.  This restatement is pinned by
-independent implementations that ARE present: torch CPU
-``scaled_dot_product_attention`` / autograd (dense forward and backward) and
-torch ``F.unfold`` / ``F.fold`` (NNlib im2col / col2im window geometry).  See
-``tests/test_oracle.py``.  The exact NNlib version the reference resolves is
-unpinned (no ``[compat]`` in Project.toml:6-19, Manifest gitignored), so window
-geometry parity is pinned to NNlib's documented ``unfold``/``fold`` semantics
-(cross-correlation order, ``flipped=true``), cross-checked against torch.
+Parity pinning — "parity unpinned" by reference-executed vectors
+-------------------------------------------------------------------
+The reference is Julia and cannot run here (no Julia, no NNlib), its C++
+counterpart needs Eigen3 (absent: unbuildable), and it ships no golden
+vectors or known-answer tests.  So no value in
+tests/golden/ was produced by the reference itself: parity is UNPINNED in
+that strict sense.  What this restatement IS checked against
+(tests/test_oracle.py):
+  * the reference's own test relations — dense_fa ≈ dense_dpa ≈
+    NNlib.dot_product_attention (test/test.jl:19-20, bench/compare.jl:20,47),
+    with torch CPU ``scaled_dot_product_attention`` standing in for NNlib;
+  * the backward against torch autograd (the reference has no backward test);
+  * window geometry against torch ``F.unfold`` / ``F.fold`` (NNlib im2col /
+    col2im with cross-correlation order, ``flipped=true``; the NNlib version is
+    unpinned: no ``[compat]`` in Project.toml:6-19, Manifest gitignored).
 """
 from __future__ import annotations
 
