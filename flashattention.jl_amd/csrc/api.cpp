@@ -89,6 +89,13 @@ int fa_debug_set_bwd_generic(int v) {
     return old;
 }
 
+// Not part of the public header: 1 forces the composed windowed forward.
+int fa_debug_set_win_composed(int v) {
+    const int old = fa::g_win_force_composed;
+    fa::g_win_force_composed = v != 0;
+    return old;
+}
+
 int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
                  int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch, float scale,
                  void* hip_stream) {

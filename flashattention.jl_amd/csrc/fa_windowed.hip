@@ -18,6 +18,8 @@
 //   fold    : deterministic per-pixel sum over covering windows (÷ count).
 // The backward is the exact chain rule: dyw = window(dy ./ count), dense
 // backward per window, fold (sum) of dqw / dkw / dvw.
+#include <type_traits>
+
 #include "fa_common.h"
 #include "fa_internal.h"
 #include "../../include/fa_hip.h"
@@ -133,11 +135,208 @@ __global__ __launch_bounds__(256) void win_fold(const T* __restrict__ src, T* __
     dst[e] = (T)acc;
 }
 
+
+// --------------------------------------------------------------------------
+// Fused single-pass windowed forward (bf16 / fp16, T <= 64 tokens per window,
+// d, dv <= 64): one wave per window, 4 windows per workgroup.
+//
+// The window's pixel indices go to a 64-entry LDS table; Q, K and V are then
+// gathered straight from the image into MFMA fragment registers with buffer
+// loads (the zero-padding pixels read as 0 through an out-of-range offset), so
+// no window batch is ever materialised in HBM.  Scores are the transposed
+// tile Sᵀ = K·Qᵀ (keys on accumulator rows, natural key order), softmax is
+// exact per window (all keys in registers: max over 2 key blocks + one
+// permlane swap), and Oᵀ = Vᵀ·Pᵀ takes P straight from the accumulator.
+// Query blocks of 32 are processed one after the other to bound registers.
+// Output: stride >= ws (no overlap) stores y directly (each covered pixel has
+// exactly one owner window; uncovered pixels are NaN-filled separately), else
+// the window outputs go to the workspace and win_fold sums / divides.
+// --------------------------------------------------------------------------
+template <class T, int D, int DV, int NKB, bool DIRECT>
+__global__ __launch_bounds__(256, 2) void win_fused(const T* __restrict__ q, const T* __restrict__ k,
+                                                    const T* __restrict__ v, T* __restrict__ out,
+                                                    float* __restrict__ lo, float* __restrict__ mo,
+                                                    WinDev g, int d, int dv, int batch, float scale,
+                                                    float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    __shared__ int ptab[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + wave;       // global window id (w + L·b)
+    const bool live = wid < (int64_t)g.L * batch;
+    const int w = live ? (int)(wid % g.L) : 0;
+    const int b = live ? (int)(wid / g.L) : 0;
+    ptab[wave][lane] = (live && lane < g.T) ? win_pixel(g, w, lane) : -1;
+    __syncthreads();
+    const int* tab = ptab[wave];
+    constexpr unsigned kOOB = 0x7FFFFFF0u;                      // past any slab: buffer load → 0
+    const auto qrs = __builtin_amdgcn_make_buffer_rsrc((void*)(q + (int64_t)b * d * g.P), (short)0, d * g.P * 2, 0x00020000);
+    const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(k + (int64_t)b * d * g.P), (short)0, d * g.P * 2, 0x00020000);
+    const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)(v + (int64_t)b * dv * g.P), (short)0, dv * g.P * 2, 0x00020000);
+    auto off = [&](int f, int pix) -> unsigned { return pix < 0 ? kOOB : (unsigned)((f * g.P + pix) * 2); };
+    auto ld = [&](__amdgpu_buffer_rsrc_t rs, unsigned o) -> T {
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(rs, o, 0, 0));
+    };
+
+    // K: A operand of Sᵀ (row = key kb·32 + r), V: A operand of Oᵀ (row = feature)
+    F8 kf[NKB][D / 16], vf[DV / 32][NKB][2];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+        const int pk = tab[kb * 32 + r];
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) kf[kb][s][e] = ld(krs, off(16 * s + 8 * h + e, pk));
+    }
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            // B-operand k order of the accumulator: element j of half h ↔ row 16s + 8(j>>2) + 4h + (j&3)
+            int pv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pv[j] = tab[kb * 32 + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3)];
+#pragma unroll
+            for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) vf[cb][kb][s][j] = ld(vrs, off(cb * 32 + r, pv[j]));
+        }
+
+    const int T_ = g.T;
+#pragma unroll
+    for (int qb = 0; qb < NKB; ++qb) {
+        const int tq = qb * 32 + r;                 // this lane's query token
+        const int pq = tab[tq];
+        F8 qf[D / 16];
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qf[s][e] = ld(qrs, off(16 * s + 8 * h + e, pq));
+        f32x16 sa[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sa[kb][x] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) sa[kb] = mfma32x32x16(kf[kb][s], qf[s], sa[kb]);
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                if (kb * 32 + acc_row(x, h) >= T_) sa[kb][x] = kNegInf;   // tokens past the window
+        }
+        float pm[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sa[kb][x]);
+        const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+        const float mc = mt * scale_log2;
+        float ps[4] = {0.f, 0.f, 0.f, 0.f};
+        F8 pf[NKB][2];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = exp2_fast(fmaf(sa[kb][x], scale_log2, -mc));
+                ps[x & 3] += pr;
+                pf[kb][x >> 3][x & 7] = (T)pr;
+            }
+        const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+        const float inv = 1.0f / lt;
+        f32x16 oa[DV / 32];
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oa[cb][x] = 0.0f;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) oa[cb] = mfma32x32x16(vf[cb][kb][s], pf[kb][s], oa[cb]);
+        }
+        if (live && tq < T_) {
+            if (h == 0) {
+                const int64_t li = tq + (int64_t)T_ * wid;
+                mo[li] = mt * scale;
+                lo[li] = lt;
+            }
+            if constexpr (DIRECT) {
+                if (pq >= 0) {
+                    T* yb = out + (int64_t)b * dv * g.P + pq;
+#pragma unroll
+                    for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                        for (int x = 0; x < 16; ++x) {
+                            const int cc = cb * 32 + acc_row(x, h);
+                            if (cc < dv) yb[(int64_t)cc * g.P] = (T)(oa[cb][x] * inv);
+                        }
+                }
+            } else {
+                T* ob = out + (int64_t)T_ * dv * wid + tq;      // (T, dv, L·B) window batch
+#pragma unroll
+                for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) {
+                        const int cc = cb * 32 + acc_row(x, h);
+                        if (cc < dv) ob[(int64_t)cc * T_] = (T)(oa[cb][x] * inv);
+                    }
+            }
+        }
+    }
+}
+
+// NaN for pixels no window covers (reference 0/0, Appendix A.7); DIRECT mode only
+template <class T>
+__global__ __launch_bounds__(256) void win_nan_uncovered(T* __restrict__ y, int dv, int64_t total, WinDev g) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int pix = (int)(e % g.P);
+    if (win_count(g, pix) == 0) y[e] = (T)__builtin_nanf("");
+}
+
+static bool fully_covered(const WindowGeom& g) {
+    for (int i = 0; i < g.nsp; ++i) {
+        if (g.stride > g.ws) return false;                                  // gaps between windows
+        if (-g.pad > 0) return false;
+        if ((g.O[i] - 1) * g.stride - g.pad + g.ws - 1 < g.S[i] - 1) return false;   // uncovered tail
+    }
+    return true;
+}
+
+int g_win_force_composed = 0;   // benchmark knob
+
+// The ONE place the fused-vs-composed decision is made: both the workspace
+// query and the launcher call it, so they can never disagree.
+static bool fused_ok(int dtype, const WindowGeom& g, int64_t d, int64_t dv) {
+    return !g_win_force_composed && dtype != FA_DTYPE_F32 && g.T <= 64 && d <= 64 && dv <= 64 &&
+           g.P * (d > dv ? d : dv) * 2 < INT32_MAX;
+}
+
+template <class T, int D, int DV>
+static hipError_t launch_fused_dd(const WindowedArgs& a, const WinDev& g, void* out, bool direct, hipStream_t s) {
+    const int64_t nw = a.g.L * a.batch;
+    const dim3 grid((unsigned)((nw + 3) / 4)), blk(256);
+    const float c = a.scale * kLog2e;
+#define FA_FUSED(NKB, DIR) hipLaunchKernelGGL((win_fused<T, D, DV, NKB, DIR>), grid, blk, 0, s, (const T*)a.q, \
+        (const T*)a.k, (const T*)a.v, (T*)out, a.l, a.m, g, (int)a.d, (int)a.dv, (int)a.batch, a.scale, c)
+    if (a.g.T <= 32) { if (direct) FA_FUSED(1, true); else FA_FUSED(1, false); }
+    else { if (direct) FA_FUSED(2, true); else FA_FUSED(2, false); }
+#undef FA_FUSED
+    return hipGetLastError();
+}
+template <class T>
+static hipError_t launch_fused(const WindowedArgs& a, const WinDev& g, void* out, bool direct, hipStream_t s) {
+    const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
+    if (Dc == 32 && DVc == 32) return launch_fused_dd<T, 32, 32>(a, g, out, direct, s);
+    if (Dc == 32) return launch_fused_dd<T, 32, 64>(a, g, out, direct, s);
+    if (DVc == 32) return launch_fused_dd<T, 64, 32>(a, g, out, direct, s);
+    return launch_fused_dd<T, 64, 64>(a, g, out, direct, s);
+}
+
 static size_t esize(int dtype) { return dtype == FA_DTYPE_F32 ? 4 : 2; }
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
     const size_t tok = (size_t)(g.T * g.L * batch);
+    if (fused_ok(dtype, g, d, dv))   // direct (no overlap): nothing; overlap: the window outputs
+        return g.stride >= g.ws ? 0 : align256(tok * dv * esize(dtype)) + 256;
     return align256(tok * d * esize(dtype)) * 2 + align256(tok * dv * esize(dtype)) * 2 + 256;
 }
 
@@ -175,6 +374,32 @@ static bool geom_fits(const WindowGeom& g, int64_t d, int64_t dv, int64_t batch)
 template <class T>
 static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char** why) {
     const WinDev g = to_dev(a.g);
+    if (a.workspace_bytes < windowed_fwd_workspace(a.dtype, a.g, a.d, a.dv, a.batch)) {
+        *why = "workspace smaller than fa_windowed_fwd_workspace()";
+        return FA_ERR_WORKSPACE;
+    }
+    if constexpr (!std::is_same<T, float>::value) {
+    if (fused_ok(a.dtype, a.g, a.d, a.dv)) {
+        hipError_t e;
+        if (a.g.stride >= a.g.ws) {
+            if ((e = launch_fused<T>(a, g, a.y, true, s)) != hipSuccess) { *why = hipGetErrorString(e); return FA_ERR_HIP; }
+            if (!fully_covered(a.g)) {
+                const int64_t total = a.g.P * a.dv * a.batch;
+                hipLaunchKernelGGL(win_nan_uncovered<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                                   (T*)a.y, (int)a.dv, total, g);
+                if ((e = hipGetLastError()) != hipSuccess) { *why = hipGetErrorString(e); return FA_ERR_HIP; }
+            }
+        } else {
+            void* ow = (void*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
+            if ((e = launch_fused<T>(a, g, ow, false, s)) != hipSuccess ||
+                (e = fold<T>(ow, a.y, (int)a.dv, a.batch, g, true, s)) != hipSuccess) {
+                *why = hipGetErrorString(e);
+                return FA_ERR_HIP;
+            }
+        }
+        return FA_OK;
+    }
+    }
     const int64_t tok = a.g.T * a.g.L * a.batch;
     char* ws = (char*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
     void* qw = ws;  ws += align256(tok * a.d * sizeof(T));
