@@ -59,7 +59,6 @@ struct FwdParams {
     float* m;
     int N, Nk, d, dv;
     int nqb, total_wg;
-    int ablate;   // TEMP experiment bits
     float scale, scale_log2;
     int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
 };
@@ -610,11 +609,11 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         F8 pf[NQB][NKB][2];
 #pragma unroll
         for (int u = 0; u < NQB; ++u) {
-            float pm[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+            float pm[4] = {sacc[u][0][0], sacc[u][0][1], sacc[u][0][2], sacc[u][0][3]};
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-                for (int x = 0; x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sacc[u][kb][x]);
+                for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sacc[u][kb][x]);
             const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
             m_true[u] = fmaxf(m_true[u], mt);
             if (__builtin_amdgcn_ballot_w64(mt > m_used[u] + thr_raw) != 0) {
@@ -700,353 +699,6 @@ __global__ __launch_bounds__(256, 2) void dense_fwd_w4q2(FwdParams p) { dense_fw
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
 
-// Scheduler pattern: K x [1 MFMA, up to 2 LDS reads] with R reads in total.
-template <int K, int R>
-__device__ __forceinline__ void mfma_ds_pattern() {
-    if constexpr (K > 0) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if constexpr (R >= 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        else if constexpr (R == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        mfma_ds_pattern<K - 1, (R >= 2 ? R - 2 : 0)>();
-    }
-}
-
-// --------------------------------------------------------------------------
-// Ping-pong forward (bf16 / fp16 fast path).  8 waves; each wave owns 32 query
-// rows.  Every wave runs the same stream of alternating segments
-//     M_j = { store tile j+1 to LDS,  Sᵀ(j) = K(j)·Qᵀ,  Oᵀ += Vᵀ(j−1)·Pᵀ(j−1) }  (MFMA)
-//     V_j = { issue global loads of tile j+2,  online softmax S(j) → P(j) }     (VALU)
-// with a barrier after every segment.  Waves 4-7 (group B) take one extra
-// barrier before starting, so they run one segment behind waves 0-3 (group A):
-// on every SIMD (waves w and w+4 share one) one wave is in a matrix segment
-// while its partner is in a vector segment.
-// LDS ring of 3 tile slots.  Group A runs M_j in barrier interval 2j, group B
-// in 2j+1; tile t is written in M_{t−1} (intervals 2t−2 / 2t−1), is complete
-// at the start of interval 2t, and is last read by group B's M_{t+1}
-// (PV(t), interval 2t+3) — before tile t+3 reuses slot t%3 in interval 2t+4.
-// --------------------------------------------------------------------------
-template <class T, int D, int DV, bool PF>
-__device__ __forceinline__ void dense_fwd_pingpong(const FwdParams& p) {
-    // LDS addresses are formed as (opaque per-lane base) + (uniform slot offset) +
-    // compile-time immediates, so every ds_read uses its offset field and the
-    // compiler cannot hoist one pre-added address per read into the loop.
-    typedef typename Frag8<T>::type F8;
-    typedef typename Frag8<T>::half F4;
-    constexpr int NTH = 512, BM = 256, BN = 64;
-    constexpr int KROW = BN * 2, VROW = BN * 2 + 16;
-    constexpr int KBYTES = D * KROW, VBYTES = DV * VROW, STAGE = KBYTES + VBYTES;
-    constexpr int CPR = BN / 8;
-    constexpr int KTOT = D * CPR, VTOT = DV * CPR;
-    constexpr int KCH = (KTOT + NTH - 1) / NTH, VCH = (VTOT + NTH - 1) / NTH;
-    static_assert(KTOT % NTH == 0 || KTOT < NTH, "tile split");
-    static_assert(VTOT % NTH == 0 || VTOT < NTH, "tile split");
-    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE + 16];
-
-    const int lid = xcd_remap(blockIdx.x, p.total_wg);
-    const int b = lid / p.nqb;
-    const int qb = lid - b * p.nqb;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
-    const auto qrs = slab_rsrc((const T*)p.Q + (int64_t)b * N * d, (uint32_t)(N * d * (int)sizeof(T)));
-    const auto krs = slab_rsrc((const T*)p.K + (int64_t)b * Nk * d, (uint32_t)(Nk * d * (int)sizeof(T)));
-    const auto vrs = slab_rsrc((const T*)p.V + (int64_t)b * Nk * dv, (uint32_t)(Nk * dv * (int)sizeof(T)));
-
-    const int qi = qb * BM + wave * 32 + r;
-    F8 qf[D / 16];
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-            qf[s][e] = (p.ablate & 16) ? (T)(0.01f * (e + s)) : __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(qrs, ((16 * s + 8 * h + e) * N + qi) * 2, 0, 0));
-
-    const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-    int koff[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-        koff[kb] = (8 * h + qq) * KROW + (((kb * 2 + kh) ^ (((qq >> 1) & 1) << 1)) * 32) + 8 * sig;
-    const int voff = r * VROW + 16 * h;
-
-    const bool kact = KTOT >= NTH || tid < KTOT, vact = VTOT >= NTH || tid < VTOT;
-    int kgo[KCH], kso[KCH], vgo[VCH], vso[VCH];
-#pragma unroll
-    for (int it = 0; it < KCH; ++it) {
-        const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
-        kgo[it] = kact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
-        kso[it] = kact ? f * KROW + (((pc >> 1) ^ (((f >> 1) & 1) << 1)) * 32) + (pc & 1) * 16 : -1;
-    }
-#pragma unroll
-    for (int it = 0; it < VCH; ++it) {
-        const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
-        vgo[it] = vact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
-        vso[it] = vact ? KBYTES + f * VROW + pc * 16 : -1;
-    }
-
-    const float c = p.scale_log2;
-    const float thr_raw = kRescaleLog2 / c;
-    const int NT = (Nk + BN - 1) / BN;
-    const bool ragged = (Nk % BN) != 0;
-
-    u32x4 kreg[KCH], vreg[VCH];
-    auto gload = [&](int t) {        // out-of-range tiles read as zeros (buffer bounds)
-        const int o = (p.ablate & 1) ? 0 : t * BN * 2;
-#pragma unroll
-        for (int it = 0; it < KCH; ++it) kreg[it] = __builtin_amdgcn_raw_buffer_load_b128(krs, kgo[it] + o, 0, 0);
-#pragma unroll
-        for (int it = 0; it < VCH; ++it) vreg[it] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vgo[it] + o, 0, 0);
-    };
-    auto opaque = [](int v) { asm volatile("" : "+v"(v)); return v; };
-    auto lstore = [&](int t, int slot) {
-        if (ragged && t == NT - 1) {   // dead keys of the last tile: V rows must be 0, not garbage
-#pragma unroll
-            for (int it = 0; it < VCH; ++it) {
-                const int ch = tid + NTH * it;
-                if (t * BN + (ch % CPR) * 8 >= Nk) vreg[it] = u32x4{0u, 0u, 0u, 0u};
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < KCH; ++it)
-            if (KTOT >= NTH || kact) *(u32x4*)(smem + opaque(kso[it] + slot)) = kreg[it];
-#pragma unroll
-        for (int it = 0; it < VCH; ++it)
-            if (VTOT >= NTH || vact) *(u32x4*)(smem + opaque(vso[it] + slot)) = vreg[it];
-    };
-
-    f32x16 oacc[DV / 32];
-#pragma unroll
-    for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-        for (int x = 0; x < 16; ++x) oacc[cb][x] = 0.0f;
-    f32x16 sacc[2];
-    F8 pf[2][2];
-    float m_used = kNegInf, m_true = kNegInf, l_run = 0.0f;
-
-    auto qk = [&](int slot) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            const char* kl = smem + opaque(koff[kb] + slot);
-#pragma unroll
-            for (int x = 0; x < 16; ++x) sacc[kb][x] = 0.0f;
-#pragma unroll
-            for (int s = 0; s < D / 16; ++s) {
-                const char* a = kl + 16 * s * KROW;
-                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
-                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW));
-                sacc[kb] = mfma32x32x16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), qf[s], sacc[kb]);
-            }
-        }
-    };
-    auto pv = [&](int slot) {
-        const char* vl = smem + opaque(voff + slot) + KBYTES;
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const F8 va = *(const F8*)(vl + cb * 32 * VROW + (kb * 32 + 16 * s) * 2);
-                    oacc[cb] = mfma32x32x16(va, pf[kb][s], oacc[cb]);
-                }
-    };
-    auto softmax = [&](int j, bool masked) {
-        if (masked) {
-            const int key0 = j * BN;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) {
-                    const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
-                    if (key0 + kt >= Nk) sacc[kb][x] = kNegInf;
-                }
-        }
-        float pm[4] = {sacc[0][0], sacc[0][1], sacc[0][2], sacc[0][3]};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sacc[kb][x]);
-        const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
-        m_true = fmaxf(m_true, mt);
-        if (__builtin_amdgcn_ballot_w64(mt > m_used + thr_raw) != 0) {
-            const float m_new = fmaxf(m_used, mt);
-            const float alpha = exp2_fast((m_used - m_new) * c);
-            l_run *= alpha;
-#pragma unroll
-            for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) oacc[cb][x] *= alpha;
-            m_used = m_new;
-        }
-        const float mc = m_used * c;
-        float ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const float pv_ = exp2_fast(fmaf(sacc[kb][x], c, -mc));
-                ps[x & 3] += pv_;
-                pf[kb][x >> 3][x & 7] = (T)pv_;
-            }
-        l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-    };
-
-    // Register-prefetch form (PF): a wave's V fragments for PV(j) are read in its
-    // V_j segment (the LDS is otherwise idle there), and the K fragments of QK(j)
-    // are all issued at the top of M_j, ahead of the PV MFMAs that hide them.
-    F8 kfr[2][D / 16];
-    F8 vfr[DV / 32][2][2];
-    auto kprefetch = [&](int slot) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            const char* kl = smem + opaque(koff[kb] + slot);
-#pragma unroll
-            for (int s = 0; s < D / 16; ++s) {
-                const char* a = kl + 16 * s * KROW;
-                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
-                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW));
-                kfr[kb][s] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto vprefetch = [&](int slot) {
-        const char* vl = smem + opaque(voff + slot) + KBYTES;
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) vfr[cb][kb][s] = *(const F8*)(vl + cb * 32 * VROW + (kb * 32 + 16 * s) * 2);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto qk_regs = [&]() {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-            for (int x = 0; x < 16; ++x) sacc[kb][x] = 0.0f;
-#pragma unroll
-            for (int s = 0; s < D / 16; ++s) sacc[kb] = mfma32x32x16(kfr[kb][s], qf[s], sacc[kb]);
-        }
-    };
-    auto pv_regs = [&]() {
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) oacc[cb] = mfma32x32x16(vfr[cb][kb][s], pf[kb][s], oacc[cb]);
-    };
-    // segment bodies (tile j in slot `cur`, tile j+1 goes to slot `nxt`)
-    // The LDS store of tile j+1 goes last: its vmcnt wait on the global loads
-    // (issued one segment earlier) then overlaps this segment's MFMA issue.
-    auto segM = [&](int j, int prv, int cur, int nxt, bool store_next, bool has_pv) {
-        if (PF) {
-            kprefetch(cur);
-            if (has_pv) pv_regs();
-            qk_regs();
-        } else {
-            qk(cur);
-            if (has_pv) pv(prv);
-            if (p.ablate & 128) {
-                // pin the interleave: 6 LDS reads of look-ahead, then 1 MFMA : 2 reads
-                constexpr int NR = 2 * (D / 16) * 2 + (DV / 32) * 4;   // tr + b128 reads
-                constexpr int NMF = 2 * (D / 16) + (DV / 32) * 4;
-                __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-                mfma_ds_pattern<NMF, NR - 6>();
-            }
-        }
-        if (store_next) lstore(j + 1, nxt);
-    };
-    auto segV = [&](int j, int cur, bool load_next, bool masked) {
-        if (PF) vprefetch(cur);
-        if (load_next) gload(j + 2);
-        if (p.ablate & 2) {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) pf[kb][x >> 3][x & 7] = (T)sacc[kb][x];
-        } else {
-            softmax(j, masked);
-        }
-    };
-
-    // slot byte offsets of tiles j-1, j, j+1 (rotate each iteration; uniform)
-    int s_prev = 2 * STAGE, s_cur = 0, s_next = STAGE;
-    auto rotate = [&]() { const int t = s_prev; s_prev = s_cur; s_cur = s_next; s_next = t; };
-
-    // prologue: tile 0 into slot 0, tile 1 in flight
-    gload(0);
-    lstore(0, s_cur);
-    gload(1);
-    __syncthreads();
-    if (wave >= 4) __builtin_amdgcn_s_barrier();   // group B: one segment behind
-    if ((p.ablate & 64) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-
-    // j = 0
-    segM(0, s_prev, s_cur, s_next, NT > 1, false);
-    __syncthreads();
-    segV(0, s_cur, true, ragged && NT == 1);
-    __syncthreads();
-    rotate();
-    // steady state: 1 <= j <= NT-2
-    uint64_t* tsb = (uint64_t*)p.O + ((int64_t)lid * 8 + wave) * 20;   // TEMP timing (ablate & 8)
-    for (int j = 1; j < NT - 1; ++j) {
-        const bool rec = (p.ablate & 8) && j >= 16 && j < 20;
-        uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-        if (rec) t0 = __builtin_amdgcn_s_memtime();
-        segM(j, s_prev, s_cur, s_next, true, true);
-        if (rec) t1 = __builtin_amdgcn_s_memtime();
-        __syncthreads();
-        if (rec) t2 = __builtin_amdgcn_s_memtime();
-        segV(j, s_cur, true, false);
-        if (rec) t3 = __builtin_amdgcn_s_memtime();
-        __syncthreads();
-        if (rec) {
-            t4 = __builtin_amdgcn_s_memtime();
-            if (lane == 0) {
-                uint64_t* q = tsb + (j - 16) * 5;
-                q[0] = t0; q[1] = t1; q[2] = t2; q[3] = t3; q[4] = t4;
-            }
-        }
-        rotate();
-    }
-    // j = NT-1 (the only tile that can be ragged)
-    if (NT > 1) {
-        segM(NT - 1, s_prev, s_cur, s_next, false, true);
-        __syncthreads();
-        segV(NT - 1, s_cur, false, ragged);
-        __syncthreads();
-        rotate();
-    }
-    if (PF) pv_regs(); else pv(s_prev);
-    if (wave < 4) __builtin_amdgcn_s_barrier();    // equal barrier counts for both groups
-
-    const float lt = swap_halves_sum(l_run);
-    const float inv = 1.0f / lt;
-    if (qi < N && !(p.ablate & 32)) {
-        T* Ob = (T*)p.O + (int64_t)b * N * dv;
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int cc = cb * 32 + acc_row(x, h);
-                if (cc < dv) Ob[(int64_t)cc * N + qi] = (T)(oacc[cb][x] * inv);
-            }
-        if (h == 0) {
-            p.m[(int64_t)b * N + qi] = m_true * p.scale;
-            p.l[(int64_t)b * N + qi] = lt * exp2_fast((m_used - m_true) * c);
-        }
-    }
-}
-
-template <class T, int D, int DV>
-__global__ __launch_bounds__(512, (D <= 64 && DV <= 64) ? 4 : 2) void dense_fwd_pp(FwdParams p) {
-    dense_fwd_pingpong<T, D, DV, false>(p);
-}
-template <class T, int D, int DV>
-__global__ __launch_bounds__(512, 2) void dense_fwd_pp2(FwdParams p) { dense_fwd_pingpong<T, D, DV, true>(p); }
-
 // --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
@@ -1060,7 +712,6 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         const int nw = (v == 5 || v == 7) ? 8 : 4;
         const int nqb = v >= 6 ? 2 : 1;
         FwdParams q = p;
-        { static int ab = -1; if (ab < 0) { const char* e = getenv("FA_ABLATE"); ab = e ? atoi(e) : 0; } q.ablate = ab; }
         q.nqb = (q.N + 32 * nw * nqb - 1) / (32 * nw * nqb);
         q.total_wg = q.nqb * (int)(p.total_wg / p.nqb);
         const dim3 g2((unsigned)q.total_wg);
@@ -1072,20 +723,7 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
             case 128: hipLaunchKernelGGL((KER<T, D, 128>), g2, blk, 0, s, q); break;    \
             default: return hipErrorInvalidValue;                                       \
         }
-        if (v == 8 || v == 9) {
-            q.nqb = (q.N + 255) / 256;
-            q.total_wg = q.nqb * (int)(p.total_wg / p.nqb);
-            const dim3 g3((unsigned)q.total_wg);
-            switch (DVc) {
-                case 32: if (v == 8) hipLaunchKernelGGL((dense_fwd_pp<T, D, 32>), g3, dim3(512), 0, s, q);
-                         else hipLaunchKernelGGL((dense_fwd_pp2<T, D, 32>), g3, dim3(512), 0, s, q); break;
-                case 64: if (v == 8) hipLaunchKernelGGL((dense_fwd_pp<T, D, 64>), g3, dim3(512), 0, s, q);
-                         else hipLaunchKernelGGL((dense_fwd_pp2<T, D, 64>), g3, dim3(512), 0, s, q); break;
-                case 128: if (v == 8) hipLaunchKernelGGL((dense_fwd_pp<T, D, 128>), g3, dim3(512), 0, s, q);
-                          else hipLaunchKernelGGL((dense_fwd_pp2<T, D, 128>), g3, dim3(512), 0, s, q); break;
-                default: return hipErrorInvalidValue;
-            }
-        } else if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
+        if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
         else if (v == 5) { FA_LAUNCH_T(dense_fwd_w8b64) }
         else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
         else { FA_LAUNCH_T(dense_fwd_w8q2) }
@@ -1142,7 +780,6 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
         return FA_ERR_UNSUPPORTED;
     }
     FwdParams p;
-    p.ablate = 0;
     p.Q = a.Q; p.K = a.K; p.V = a.V; p.O = a.O; p.l = a.l; p.m = a.m;
     p.N = (int)a.N; p.Nk = (int)a.Nk; p.d = (int)a.d; p.dv = (int)a.dv;
     p.nqb = (int)((a.N + kBM - 1) / kBM);

@@ -20,5 +20,5 @@ case "$STEPS" in
 esac
 rc=$?
 echo "exit $rc"
-tail -5 gpurun_out/*.log
+for f in gpurun_out/*.log; do echo "== $f"; tail -n 5 "$f"; done
 exit $rc
