@@ -206,4 +206,19 @@ int fa_windowed_bwd(int dtype, const void* q, const void* k, const void* v, cons
     return rc == FA_OK ? ok() : fail(rc, fn, why);
 }
 
+int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
+                     int64_t N, int64_t d, int64_t dv, int64_t batch, int64_t W, float scale,
+                     void* hip_stream) {
+    static const char* fn = "fa_circulant_fwd";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (N < 1 || d < 1 || dv < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, d, dv, batch must be >= 1");
+    if (W < 1) return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: window size W must be >= 1");
+    if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    fa::CircArgs a{dtype, Q, K, V, O, l, m, N, d, dv, batch, W, resolve_scale(scale, d)};
+    const char* why = "";
+    const int rc = fa::launch_circulant_fwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
 }  // extern "C"

@@ -76,6 +76,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// Lazy-rescale threshold (log2 units) of the online softmax: the running max
+// used for the exponentials is raised only when a tile exceeds it by more than
+// this, so P <= 2^kRescaleLog2 and the O/l rescale is a rare uniform branch.
+constexpr float kRescaleLog2 = 8.0f;
+
+// Buffer descriptor over one slab: out-of-range offsets read as 0.
+template <class T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const T* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
 template <class T> __device__ __forceinline__ T zero_val() { return (T)0.0f; }
 
 }  // namespace fa

@@ -452,13 +452,6 @@ __global__ __launch_bounds__(kThreads) void dense_fwd_generic_f32(FwdParams p) {
 //    exact max is tracked separately for the returned m (and l is converted to
 //    it at the end).
 // --------------------------------------------------------------------------
-constexpr float kRescaleLog2 = 8.0f;
-
-
-template <class T>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const T* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
-}
 
 // --------------------------------------------------------------------------
 // bf16 / fp16 fast path, generalised geometry: NW waves x 32 query rows per

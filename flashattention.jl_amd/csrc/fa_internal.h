@@ -62,6 +62,15 @@ struct WindowedBwdArgs {
     size_t workspace_bytes;
 };
 
+struct CircArgs {
+    int dtype;
+    const void *Q, *K, *V;
+    void* O;
+    float *l, *m;
+    int64_t N, d, dv, batch, W;
+    float scale;
+};
+
 // Each returns a hipError_t-like code through *err and a fa_status.
 int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
@@ -70,6 +79,7 @@ size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv,
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why);
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why);
+int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why);
 
 // Padded head-dim class a kernel is compiled for: 32, 64 or 128 (0 = none).
 inline int head_dim_class(int64_t d) {

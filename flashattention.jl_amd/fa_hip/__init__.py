@@ -38,7 +38,7 @@ __all__ = [
     "DimensionMismatch", "FlashAttentionError", "lib", "lib_path",
     "jl_empty", "jl_zeros", "jl_tensor", "jl_strides", "is_jl_contiguous",
     "dense_fa", "dense_fa_", "dense_fa_backward", "windowed_fa", "block_fa",
-    "windowed_fa_backward", "window_geometry", "DTYPES",
+    "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_", "DTYPES",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -111,6 +111,8 @@ def lib() -> ctypes.CDLL:
     L.fa_windowed_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                   ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64,
                                   f32, vp, ctypes.c_size_t, vp]
+    L.fa_circulant_fwd.restype = ctypes.c_int
+    L.fa_circulant_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp]
     del fp
     for dbg in ("fa_debug_set_fwd_variant", "fa_debug_set_bwd_generic"):
         if hasattr(L, dbg):
@@ -254,6 +256,44 @@ def dense_fa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float = 0
     dense_fa_(O, l, m, Q, K, V, scale)
     y = O.as_strided(tuple(q.shape[: D - 2]) + (dv, B), jl_strides(tuple(q.shape[: D - 2]) + (dv, B)))
     return y, l, m
+
+
+def circulant_fa_(O: torch.Tensor, l: torch.Tensor, m: torch.Tensor,
+                  Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, W: int,
+                  scale: float = 0.0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """``circulant_fa!(O, l, m, Q, K, V, W)`` — src/circulant.jl:9-118, in place.
+
+    Query i attends the W band keys (i - p + t) mod N, t = 0..W-1,
+    p = (W-1)÷2 (``cartesian_circulant``, src/utils.jl:6-17).  Q, K (N, d, B),
+    V (N, dv, B), O (N, dv, B), l, m (N, 1, B) float32.
+    """
+    for t in (O, l, m, Q, K, V):
+        _require(t.dim() == 3, "circulant_fa! expects 3-D (N, d, batch) arrays")
+    N, d, B = Q.shape
+    dv = V.shape[1]
+    _require(int(W) >= 1, "window size W must be >= 1")
+    _require(K.shape == (N, d, B), f"K has shape {tuple(K.shape)}, expected ({N}, {d}, {B})")
+    _require(V.shape == (N, dv, B), f"V has shape {tuple(V.shape)}, expected ({N}, {dv}, {B})")
+    _require(O.shape == (N, dv, B), f"O has shape {tuple(O.shape)}, expected ({N}, {dv}, {B})")
+    _require(l.shape == (N, 1, B) and m.shape == (N, 1, B), "l, m must be (N, 1, batch)")
+    _require(l.dtype == torch.float32 and m.dtype == torch.float32, "l, m must be float32")
+    code = _dtype_code(Q, K, V, O)
+    _device_check(Q, K, V, O, l, m)
+    _check(lib().fa_circulant_fwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
+                                  N, d, dv, B, int(W), float(scale), _stream(Q)))
+    return O, l, m
+
+
+def circulant_fa(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, W: int, scale: float = 0.0):
+    """``circulant_fa(Q, K, V, W) -> (O, l, m)`` — src/circulant.jl:1-7, with the
+    reference wrapper's defects fixed (it drops W and allocates O like Q)."""
+    _require(Q.dim() == 3 and K.dim() == 3 and V.dim() == 3, "circulant_fa expects 3-D arrays")
+    _device_check(Q, K, V)
+    N, d, B = Q.shape
+    O = jl_empty((N, V.shape[1], B), Q.dtype, Q.device)
+    l = jl_empty((N, 1, B), torch.float32, Q.device)
+    m = jl_empty((N, 1, B), torch.float32, Q.device)
+    return circulant_fa_(O, l, m, Q, K, V, W, scale)
 
 
 def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):

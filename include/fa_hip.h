@@ -129,6 +129,19 @@ int fa_windowed_bwd(int dtype,
                     float scale, void* workspace, size_t workspace_bytes,
                     void* hip_stream);
 
+/* Circulant (periodic banded) attention, replaces
+ *   circulant_fa!(O, l, m, Q, K, V, W)   reference src/circulant.jl:9-118
+ * (naive form circulant_dpa! src/naive/circulant.jl:8-36).  Query i attends
+ * the W band entries (i - p + t) mod N, t = 0..W-1, p = (W-1)/2 — the keys
+ * cartesian_circulant enumerates (src/utils.jl:6-17); W > N repeats keys.
+ * Q, K: (N, d, batch); V: (N, dv, batch); O: (N, dv, batch); l, m: (N, 1, batch)
+ * float32 with the dense_fa! meaning.  Any W >= 1 (the reference's own
+ * benchmark uses even W, bench/compare.jl:98). */
+int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V,
+                     void* O, float* l, float* m,
+                     int64_t N, int64_t d, int64_t dv, int64_t batch, int64_t W,
+                     float scale, void* hip_stream);
+
 /* Thread-local description of the last error on this host thread ("" if none). */
 const char* fa_last_error(void);
 

@@ -366,3 +366,103 @@ def windowed_fa_backward(q, k, v, dy, ws: int, stride: int | None = None,
     dk = unwindow(np.reshape(dKw, (T, d, L, B), order="F"), sp + (d, q.shape[-1]), ws, stride, pad)
     dvv = unwindow(np.reshape(dVw, (T, dv, L, B), order="F"), sp + (dv, q.shape[-1]), ws, stride, pad)
     return dq, dk, dvv
+
+
+# ---------------------------------------------------------------------------
+# circulant (periodic banded) attention — SURVEY §8f row 3
+# ---------------------------------------------------------------------------
+def circshift_index(m: int, s: int, M: int) -> int:
+    """``circshift_index(m, s, M)`` — src/utils.jl:4 (1-based)."""
+    return (m - 1 - s) % M + 1
+
+
+def cartesian_circulant(n: int, N: int, M: int) -> Tuple[int, int]:
+    """``cartesian_circulant(n, N, M)`` — src/utils.jl:6-17 (1-based (i, j)):
+    entry n of the column-major N×N circulant with M nonzeros per column."""
+    p = (M - 1) // 2
+    j = _cld(n, M)
+    m = (n - 1) % M + 1
+    if j <= p:
+        m = circshift_index(m, j - p - 1, M)
+    elif j > N - p:
+        m = circshift_index(m, p - N + j, M)
+    i = ((m - 1) + (j - 1) - p) % N + 1
+    return i, j
+
+
+def circulant_index(N: int, W: int) -> np.ndarray:
+    """0-based key index ``J[w, i]`` of band entry w of query i, exactly as the
+    reference loops compute it: ``jjj = cartesian_circulant((i-1)*W + w, N, W)[1]``
+    (src/circulant.jl:74-75, src/naive/circulant.jl:21-22)."""
+    J = np.empty((W, N), dtype=np.int64)
+    for i in range(N):
+        for w in range(W):
+            J[w, i] = cartesian_circulant(i * W + w + 1, N, W)[0] - 1
+    return J
+
+
+def circulant_dpa3(Q, K, V, W: int):
+    """``circulant_dpa!(O, P, Q, K, V, W)`` — src/naive/circulant.jl:8-36:
+    band scores P[w, i] = τ qᵢ·k_J[w,i], softmax over w (dims=1), O = Pᵀ-circulant · V.
+    Returns O (N, dv, B) and P (W, N, B)."""
+    Q = np.asarray(Q, dtype=np.float64)
+    K = np.asarray(K, dtype=np.float64)
+    V = np.asarray(V, dtype=np.float64)
+    N, d, B = Q.shape
+    dv = V.shape[1]
+    tau = 1.0 / math.sqrt(d)
+    J = circulant_index(N, W)
+    O = np.zeros((N, dv, B))
+    P = np.zeros((W, N, B))
+    for b in range(B):
+        S = tau * np.einsum("nk,wnk->wn", Q[:, :, b], K[J, :, b])   # :19-24
+        S = np.exp(S - S.max(axis=0, keepdims=True))
+        S /= S.sum(axis=0, keepdims=True)                             # softmax!(P, dims=1), :27
+        P[:, :, b] = S
+        O[:, :, b] = np.einsum("wn,wnc->nc", S, V[J, :, b])          # P * bV, :28-34
+    return O, P
+
+
+def circulant_fa3(Q, K, V, W: int, M: int = CACHE_M):
+    """Blockwise ``circulant_fa!(O, l, m, Q, K, V, W)`` — src/circulant.jl:9-118.
+
+    Tile policy Bw = clamp(cld(M, d), 1, W), Br = clamp(min(d, cld(M, d)), 1, N)
+    (:22-25); per (row block, window block) the FA-1 update of dense_fa! (:80-103)
+    with O kept normalised.  Returns O (N, dv, B), l, m (N, 1, B).  dv may differ
+    from d (the reference allocates O like Q, :3).
+    """
+    Q = np.asarray(Q, dtype=np.float64)
+    K = np.asarray(K, dtype=np.float64)
+    V = np.asarray(V, dtype=np.float64)
+    N, d, B = Q.shape
+    dv = V.shape[1]
+    Bw = min(max(_cld(M, d), 1), W)
+    Br = min(max(min(d, _cld(M, d)), 1), N)
+    tau = 1.0 / math.sqrt(d)
+    J = circulant_index(N, W)
+    O = np.zeros((N, dv, B))
+    l = np.zeros((N, 1, B))
+    m = np.full((N, 1, B), -np.inf)
+    for i in range(_cld(N, Br)):
+        r0, r1 = i * Br, min(N, (i + 1) * Br)
+        Oi = np.zeros((r1 - r0, dv, B))
+        li = np.zeros((r1 - r0, B))
+        mi = np.full((r1 - r0, B), -np.inf)
+        for w in range(_cld(W, Bw)):
+            w0, w1 = w * Bw, min(W, (w + 1) * Bw)
+            Jw = J[w0:w1, r0:r1]                                          # (nw, nr)
+            Piw = tau * np.einsum("nkb,wnkb->nwb", Q[r0:r1], K[Jw])       # :70-79
+            miw = Piw.max(axis=1)                                         # :80
+            Piw = np.exp(Piw - miw[:, None, :])                           # :81
+            liw = Piw.sum(axis=1)                                         # :82
+            mi_new = np.maximum(mi, miw)                                  # :84
+            ei = np.exp(mi - mi_new)                                      # :85
+            eiw = np.exp(miw - mi_new)                                    # :86
+            li_new = ei * li + eiw * liw                                  # :87
+            t = np.einsum("nwb,wncb->ncb", Piw, V[Jw])                    # :90-100
+            Oi = ((li * ei)[:, None, :] * Oi + eiw[:, None, :] * t) / li_new[:, None, :]   # :101
+            li, mi = li_new, mi_new                                       # :106-107
+        O[r0:r1] = Oi
+        l[r0:r1, 0] = li
+        m[r0:r1, 0] = mi
+    return O, l, m

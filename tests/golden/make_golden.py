@@ -91,8 +91,29 @@ WINDOWED = [
     ("wind_3d_6x5x4_ws3_s2", (6, 5, 4), 8, 8, 1, 3, 2, 1, 37),
 ]
 
+CIRCULANT = [
+    # name, N, d, dv, B, W, seed           (src/circulant.jl:9-118)
+    ("circ_n30_w7_d12_dv6", 30, 12, 6, 2, 7, 41),        # N % 8 != 0: generic path
+    ("circ_n64_w16_d32", 64, 32, 32, 1, 16, 42),         # even W (bench/compare.jl:98 uses W+1)
+    ("circ_n20_w29_d8", 20, 8, 8, 1, 29, 43),            # W > N: keys repeat
+    ("circ_n40_w57_d16", 40, 16, 16, 1, 57, 44),         # W > N on the tiled path
+    ("circ_n256_w129_d64", 256, 64, 64, 2, 129, 45),     # reference bench window 128 + 1
+    ("circ_n200_w1_d32_dv16", 200, 32, 16, 1, 1, 46),    # W = 1: O = V
+    ("circ_n136_w64_d128_dv96", 136, 128, 96, 1, 64, 47),  # partial last workgroup
+]
 
-def main():
+
+def main(which=("dense", "backward", "windowed", "circulant")):
+    if "circulant" in which:
+        for name, N, d, dv, B, W, seed in CIRCULANT:
+            rng = np.random.default_rng(seed)
+            Q = gen(rng, (N, d, B)); K = gen(rng, (N, d, B)); V = gen(rng, (N, dv, B))
+            Oo, l, m = O.circulant_fa3(Q, K, V, W)
+            O2, _ = O.circulant_dpa3(Q, K, V, W)
+            assert np.allclose(Oo, O2, rtol=1e-12, atol=1e-12)
+            print(save(name, in_q=Q, in_k=K, in_v=V, o=Oo, l=l, m=m, W=np.int64(W)))
+    if "dense" not in which:
+        return
     for name, spq, spk, d, dv, B, kind, seed in DENSE:
         rng = np.random.default_rng(seed)
         q = gen(rng, spq + (d, B), kind)
@@ -102,6 +123,8 @@ def main():
         y2, _ = O.dense_dpa(q, k, v)
         assert np.allclose(y, y2, rtol=1e-12, atol=1e-12)
         print(save(name, in_q=q, in_k=k, in_v=v, y=y, l=l, m=m))
+    if "backward" not in which:
+        return
     for name, N, Nk, d, dv, B, seed in BACKWARD:
         rng = np.random.default_rng(seed)
         Q = gen(rng, (N, d, B)); K = gen(rng, (Nk, d, B)); V = gen(rng, (Nk, dv, B))
@@ -109,6 +132,8 @@ def main():
         Oo, l, m = O.dense_fa3(Q, K, V)
         dQ, dK, dV = O.dense_fa_backward(Q, K, V, Oo, dO, l, m)
         print(save(name, in_q=Q, in_k=K, in_v=V, in_do=dO, o=Oo, l=l, m=m, dq=dQ, dk=dK, dv=dV))
+    if "windowed" not in which:
+        return
     for name, sp, d, dv, B, ws, stride, pad, seed in WINDOWED:
         rng = np.random.default_rng(seed)
         q = gen(rng, sp + (d, B)); k = gen(rng, sp + (d, B)); v = gen(rng, sp + (dv, B))
@@ -124,4 +149,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(tuple(sys.argv[1:]) or ("dense", "backward", "windowed", "circulant"))

@@ -27,7 +27,7 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("fa_dense_fwd", "fa_dense_bwd", "fa_dense_bwd_workspace", "fa_windowed_fwd",
               "fa_windowed_fwd_workspace", "fa_windowed_bwd", "fa_windowed_workspace",
-              "fa_last_error", "fa_abi_version", "fa_max_head_dim"):
+              "fa_circulant_fwd", "fa_last_error", "fa_abi_version", "fa_max_head_dim"):
         assert f in fns
 
 
@@ -76,6 +76,13 @@ def test_invalid_arguments_return_status_and_message():
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"window" in L.fa_last_error()
     rc = L.fa_windowed_fwd(1, P, P, P, P, P, P, 4, sp, 4, 4, 1, 3, 3, 0, 0.0, None, 0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"nspatial" in L.fa_last_error()
+    # circulant: band width and head dim validated before any launch
+    rc = L.fa_circulant_fwd(1, P, P, P, P, P, P, 64, 32, 32, 1, 0, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"window size" in L.fa_last_error()
+    rc = L.fa_circulant_fwd(1, P, P, P, P, P, P, 64, 129, 32, 1, 7, 0.0, None)
+    assert rc == fa_hip.FA_ERR_UNSUPPORTED and b"head dimension" in L.fa_last_error()
+    rc = L.fa_circulant_fwd(1, P, None, P, P, P, P, 64, 32, 32, 1, 7, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"null" in L.fa_last_error()
     # backward: workspace check happens before any launch
     need = L.fa_dense_bwd_workspace(1, 128, 128, 64, 64, 2)
     if need > 0:
@@ -117,6 +124,12 @@ def test_python_mirror_shape_checks_raise_dimension_mismatch():
         fa_hip.windowed_fa(fa_hip.jl_empty((4, 4, 2, 1), device="cpu"),
                            fa_hip.jl_empty((4, 4, 2, 1), device="cpu"),
                            fa_hip.jl_empty((4, 4, 2, 1), device="cpu"), 9, stride=9, pad=0)
+    with pytest.raises(fa_hip.DimensionMismatch):
+        fa_hip.circulant_fa_(O, l, l, Q, K, Q, 3)
+    with pytest.raises(fa_hip.DimensionMismatch):
+        fa_hip.circulant_fa_(O, l, l, Q, Q, Q, 0)
+    with pytest.raises(TypeError, match="no CPU fallback"):
+        fa_hip.circulant_fa(Q, Q, Q, 3)
 
 
 def test_julia_layout_helpers():

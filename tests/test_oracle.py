@@ -176,3 +176,58 @@ def test_cpu_port_matches_oracle(path):
                                       r(g["v"]).astype(np.float32), nthreads=2)
     assert np.abs(O32 - r(g["y"])).max() < 1e-5
     assert D >= 3
+
+
+# --- circulant (src/circulant.jl, src/naive/circulant.jl, src/utils.jl:4-17) ---
+@pytest.mark.parametrize("N,W", [(10, 3), (10, 4), (30, 7), (20, 29), (64, 16), (5, 12), (9, 1)])
+def test_cartesian_circulant_is_the_periodic_band(N, W):
+    """cartesian_circulant enumerates, for column i, the band (i − p + t) mod N,
+    t = 0..W−1 (with multiplicity when W > N); for odd W <= N (the reference's
+    precondition, src/utils.jl:7) the circshift makes the rows come out sorted."""
+    J = O.circulant_index(N, W)
+    p = (W - 1) // 2
+    for i in range(N):
+        band = sorted((i - p + t) % N for t in range(W))
+        assert sorted(J[:, i].tolist()) == band
+        if W <= N and W % 2 == 1:
+            assert list(J[:, i]) == sorted(J[:, i])      # CSC rowvals come out sorted
+
+
+def _torch_band_sdpa(Q, K, V, W):
+    """Independent restatement: dense SDPA with an additive band mask (torch CPU)."""
+    N, d, B = Q.shape
+    p = (W - 1) // 2
+    out = np.zeros((N, V.shape[1], B))
+    i = np.arange(N)[:, None]
+    for b in range(B):
+        # multiplicity: count how many band entries t hit key j
+        cnt = np.zeros((N, N))
+        for t in range(W):
+            np.add.at(cnt, (np.arange(N), (np.arange(N) - p + t) % N), 1.0)
+        bias = np.where(cnt > 0, np.log(np.maximum(cnt, 1e-300)), -np.inf)
+        s = torch.tensor(Q[:, :, b]) @ torch.tensor(K[:, :, b]).T / math.sqrt(d) + torch.tensor(bias)
+        out[:, :, b] = (torch.softmax(s, dim=1) @ torch.tensor(V[:, :, b])).numpy()
+    return out
+
+
+@pytest.mark.parametrize("N,d,dv,W", [(30, 12, 6, 7), (64, 32, 32, 16), (20, 8, 8, 29), (100, 16, 8, 1)])
+def test_circulant_fa_equals_dpa_and_band_sdpa(N, d, dv, W):
+    rng = np.random.default_rng(N + W)
+    Q, K, V = rng.standard_normal((N, d, 2)), rng.standard_normal((N, d, 2)), rng.standard_normal((N, dv, 2))
+    Of, l, m = O.circulant_fa3(Q, K, V, W, M=64)          # small M: several window blocks
+    Od, P = O.circulant_dpa3(Q, K, V, W)
+    assert np.allclose(Of, Od, atol=1e-12)
+    assert np.allclose(P.sum(axis=0), 1.0)
+    assert np.allclose(Of, _torch_band_sdpa(Q, K, V, W), atol=1e-10)
+    J = O.circulant_index(N, W)
+    S = np.einsum("nkb,wnkb->wnb", Q, K[J]) / math.sqrt(d)
+    assert np.allclose(m[:, 0], S.max(axis=0)) and np.allclose(l[:, 0], np.exp(S - S.max(axis=0)).sum(axis=0))
+
+
+@pytest.mark.parametrize("path", golden_files("circ_"))
+def test_golden_circulant_reproduces(path):
+    g = load_golden(path)
+    W = int(g["W"])
+    Oo, l, m = O.circulant_fa3(g["q"], g["k"], g["v"], W)
+    assert np.allclose(Oo, g["o"], atol=1e-6)
+    assert np.allclose(l, g["l"], rtol=1e-12) and np.allclose(m, g["m"], rtol=1e-12, atol=1e-12)
