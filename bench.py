@@ -228,6 +228,20 @@ def extra_benches(fa_hip, args, dist):
             res[f"cfg3_windowed_B{Bimg}_us"] = t * 1e6
         except fa_hip.FlashAttentionError as ex:
             res[f"cfg3_windowed_B{Bimg}"] = str(ex)
+    # circulant: the reference's runcirculant shape
+    # (bench/compare.jl:105-115: N=4096, d=32, bs=1, W = 16..256) and a
+    # device-scale shape (B·H=64, N=16384, d=64, W=129; HBM-bound, GB/s)
+    for (Nc, dc, Bc, Wc) in ((4096, 32, 1, 16), (4096, 32, 1, 256), (16384, 64, 64, 129)):
+        Qc, Kc, Vc = (_randn_jl(fa_hip, (Nc, dc, Bc), torch.bfloat16, gen) for _ in range(3))
+        Oc = fa_hip.jl_empty((Nc, dc, Bc), torch.bfloat16)
+        lc = fa_hip.jl_empty((Nc, 1, Bc)); mc = fa_hip.jl_empty((Nc, 1, Bc))
+        steps = args.steps
+        w, e = time_launches(lambda: fa_hip.circulant_fa_(Oc, lc, mc, Qc, Kc, Vc, Wc), steps, 2, dist)
+        t = e / steps
+        tag = f"circ_N{Nc}_d{dc}_B{Bc}_W{Wc}"
+        res[f"{tag}_us"] = t * 1e6
+        res[f"{tag}_GBs"] = Bc * Nc * (4 * dc * 2 + 8) / t / 1e9       # Q, K, V, O + l, m
+        res[f"{tag}_tflops"] = 4.0 * Bc * Nc * Wc * dc / t / 1e12
     return res
 
 

@@ -106,3 +106,27 @@ end
 # block_fa — src/windowed.jl:1
 block_fa(q::ROCArray, k::ROCArray, v::ROCArray, windowsize; pad=0) =
     windowed_fa(q, k, v, windowsize; stride=windowsize, pad=pad)
+
+# circulant_fa!(O, l, m, Q, K, V, W) — replaces src/circulant.jl:9-118
+function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
+    N, d, B = size(Q)
+    dv = size(V, 2)
+    size(K) == (N, d, B) || throw(DimensionMismatch("K"))
+    size(V) == (N, dv, B) || throw(DimensionMismatch("V"))
+    size(O) == (N, dv, B) || throw(DimensionMismatch("O"))
+    fa_check(ccall((:fa_circulant_fwd, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                    Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
+                   fa_dtype(T), Q, K, V, O, l, m, N, d, dv, B, W, 0f0, stream_ptr()))
+    return O, l, m
+end
+
+# circulant_fa(Q, K, V, W) — src/circulant.jl:1-7, passing W (the reference call drops it)
+function circulant_fa(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
+    N, _, B = size(Q)
+    O = similar(V, N, size(V, 2), B)
+    l = similar(Q, Float32, N, 1, B)
+    m = similar(Q, Float32, N, 1, B)
+    return circulant_fa!(O, l, m, Q, K, V, W)
+end
