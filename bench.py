@@ -242,6 +242,17 @@ def extra_benches(fa_hip, args, dist):
         res[f"{tag}_us"] = t * 1e6
         res[f"{tag}_GBs"] = Bc * Nc * (4 * dc * 2 + 8) / t / 1e9       # Q, K, V, O + l, m
         res[f"{tag}_tflops"] = 4.0 * Bc * Nc * Wc * dc / t / 1e12
+    del Qc, Kc, Vc, Oc
+    # fused softmax: a configs[1]-shaped score tensor
+    # (4096 x 4096 x 64 bf16, 2 GiB) along each dim; HBM-bound: read + write
+    Ssm = _randn_jl(fa_hip, (4096, 4096, 64), torch.bfloat16, gen)
+    Psm = torch.empty_like(Ssm)
+    for dims in (1, 2):
+        steps = max(3, args.steps // 4)
+        w, e = time_launches(lambda: fa_hip.fused_softmax_(Psm, Ssm, dims), steps, 1, dist)
+        t = e / steps
+        res[f"softmax_4096x4096x64_dims{dims}_GBs"] = 2 * Ssm.numel() * 2 / t / 1e9
+        res[f"softmax_4096x4096x64_dims{dims}_us"] = t * 1e6
     return res
 
 

@@ -221,4 +221,26 @@ int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V, voi
     return rc == FA_OK ? ok() : fail(rc, fn, why);
 }
 
+size_t fa_softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims) {
+    if (M < 1 || N < 1 || batch < 1 || (dims != 1 && dims != 2)) return 0;
+    return fa::softmax_workspace(M, N, batch, dims);
+}
+
+int fa_softmax(int dtype, const void* S, void* P, int64_t M, int64_t N, int64_t batch, int dims,
+               void* workspace, size_t workspace_bytes, void* hip_stream) {
+    static const char* fn = "fa_softmax";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (dims != 1 && dims != 2) return fail(FA_ERR_INVALID_ARG, fn, "only softmax in dims 1 or 2 supported");
+    if (M < 1 || N < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: M, N, batch must be >= 1");
+    if (!S || !P) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    const size_t need = fa::softmax_workspace(M, N, batch, dims);
+    if (need > 0 && (!workspace || workspace_bytes < need))
+        return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_softmax_workspace()");
+    fa::SoftmaxArgs a{dtype, S, P, M, N, batch, dims, workspace, workspace_bytes};
+    const char* why = "";
+    const int rc = fa::launch_softmax(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
 }  // extern "C"

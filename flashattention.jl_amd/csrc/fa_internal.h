@@ -71,6 +71,16 @@ struct CircArgs {
     float scale;
 };
 
+struct SoftmaxArgs {
+    int dtype;
+    const void* S;
+    void* P;
+    int64_t M, N, batch;
+    int dims;                  // 1: over M (contiguous), 2: over N (stride M)
+    void* workspace;
+    size_t workspace_bytes;
+};
+
 // Each returns a hipError_t-like code through *err and a fa_status.
 int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
@@ -80,6 +90,8 @@ size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why);
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why);
 int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why);
+size_t softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims);
+int launch_softmax(const SoftmaxArgs& a, hipStream_t s, const char** why);
 
 // Padded head-dim class a kernel is compiled for: 32, 64 or 128 (0 = none).
 inline int head_dim_class(int64_t d) {

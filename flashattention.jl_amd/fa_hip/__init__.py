@@ -38,7 +38,8 @@ __all__ = [
     "DimensionMismatch", "FlashAttentionError", "lib", "lib_path",
     "jl_empty", "jl_zeros", "jl_tensor", "jl_strides", "is_jl_contiguous",
     "dense_fa", "dense_fa_", "dense_fa_backward", "windowed_fa", "block_fa",
-    "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_", "DTYPES",
+    "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_",
+    "fused_softmax", "fused_softmax_", "DTYPES",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -113,6 +114,10 @@ def lib() -> ctypes.CDLL:
                                   f32, vp, ctypes.c_size_t, vp]
     L.fa_circulant_fwd.restype = ctypes.c_int
     L.fa_circulant_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp]
+    L.fa_softmax_workspace.restype = ctypes.c_size_t
+    L.fa_softmax_workspace.argtypes = [i64, i64, i64, ctypes.c_int]
+    L.fa_softmax.restype = ctypes.c_int
+    L.fa_softmax.argtypes = [ctypes.c_int, vp, vp, i64, i64, i64, ctypes.c_int, vp, ctypes.c_size_t, vp]
     del fp
     for dbg in ("fa_debug_set_fwd_variant", "fa_debug_set_bwd_generic"):
         if hasattr(L, dbg):
@@ -294,6 +299,33 @@ def circulant_fa(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, W: int, scal
     l = jl_empty((N, 1, B), torch.float32, Q.device)
     m = jl_empty((N, 1, B), torch.float32, Q.device)
     return circulant_fa_(O, l, m, Q, K, V, W, scale)
+
+
+def fused_softmax_(P: torch.Tensor, S: torch.Tensor, dims: int = 1) -> torch.Tensor:
+    """``fused_softmax!(P, S; dims)`` — src/fused_softmax.jl:1-41 (device versions
+    src/cuda/fused_softmax.jl:11-314), in place into P (P may be S).
+
+    S, P: vector (M,), matrix (M, N) or (M, N, batch), Julia column-major;
+    dims = 1 normalises columns (first dim), dims = 2 rows (second dim).
+    """
+    _require(dims in (1, 2), "only softmax in dims 1 or 2 supported")
+    _require(S.dim() in (1, 2, 3) and P.shape == S.shape, "P and S must have the same 1-, 2- or 3-D shape")
+    _require(S.dim() >= 2 or dims == 1, "a vector is softmaxed along dims = 1")
+    shp = tuple(S.shape) + (1,) * (3 - S.dim())
+    M, N, B = shp
+    code = _dtype_code(S, P)
+    _device_check(S, P)
+    _require(is_jl_contiguous(S) and is_jl_contiguous(P), "S and P must be Julia column-major contiguous")
+    ws = lib().fa_softmax_workspace(M, N, B, dims)
+    buf = _workspace(S.device, ws) if ws else None
+    _check(lib().fa_softmax(code, _ptr(S), _ptr(P), M, N, B, dims, _ptr(buf), ws, _stream(S)))
+    return P
+
+
+def fused_softmax(S: torch.Tensor, dims: int = 1) -> torch.Tensor:
+    """``fused_softmax(S; dims=1)`` — src/fused_softmax.jl:1."""
+    P = torch.empty_strided(S.shape, S.stride(), dtype=S.dtype, device=S.device)
+    return fused_softmax_(P, S, dims)
 
 
 def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):

@@ -142,6 +142,18 @@ int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V,
                      int64_t N, int64_t d, int64_t dv, int64_t batch, int64_t W,
                      float scale, void* hip_stream);
 
+/* Standalone fused softmax, replaces
+ *   fused_softmax!(P, S; dims)   reference src/fused_softmax.jl:1-41
+ * (device versions src/cuda/fused_softmax.jl:11-314).  S, P: (M, N, batch)
+ * column-major, same dtype; dims = 1 normalises each column S[:, j, b]
+ * (M contiguous elements), dims = 2 each row S[i, :, b].  P may equal S
+ * (in place, fused_softmax!(S)).  A vector is (M, 1, 1) with dims = 1.
+ * Computed in fp32; an all -Inf or NaN-containing vector gives NaN, as the
+ * reference's arithmetic does. */
+size_t fa_softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims);
+int fa_softmax(int dtype, const void* S, void* P, int64_t M, int64_t N, int64_t batch, int dims,
+               void* workspace, size_t workspace_bytes, void* hip_stream);
+
 /* Thread-local description of the last error on this host thread ("" if none). */
 const char* fa_last_error(void);
 

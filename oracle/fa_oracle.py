@@ -466,3 +466,19 @@ def circulant_fa3(Q, K, V, W: int, M: int = CACHE_M):
         l[r0:r1, 0] = li
         m[r0:r1, 0] = mi
     return O, l, m
+
+
+# ---------------------------------------------------------------------------
+# standalone fused softmax — SURVEY §8f row 4
+# ---------------------------------------------------------------------------
+def fused_softmax(S, dims: int = 1):
+    """``fused_softmax(S; dims)`` — src/fused_softmax.jl:1-41: vector, matrix or
+    3-array; dims = 1 → ``col_softmax!`` (:30-41, each S[:, j, b]), dims = 2 →
+    ``row_softmax!`` (:17-28, each S[i, :, b]).  Per vector: s .- maximum(s),
+    exp, ./ sum (so an all -Inf vector, or one holding NaN / +Inf, is NaN)."""
+    assert dims in (1, 2), "only softmax in dims 1 or 2 supported"   # :12
+    S = np.asarray(S, dtype=np.float64)
+    ax = dims - 1
+    with np.errstate(invalid="ignore", over="ignore"):
+        num = np.exp(S - S.max(axis=ax, keepdims=True))
+        return num / num.sum(axis=ax, keepdims=True)

@@ -102,8 +102,22 @@ CIRCULANT = [
     ("circ_n136_w64_d128_dv96", 136, 128, 96, 1, 64, 47),  # partial last workgroup
 ]
 
+SOFTMAX = [
+    # name, shape (M, N, B), dims, seed      (src/fused_softmax.jl:1-41)
+    ("softmax_cols_37x5x2", (37, 5, 2), 1, 51),
+    ("softmax_rows_37x5x2", (37, 5, 2), 2, 52),
+    ("softmax_rows_300x70x1", (300, 70, 1), 2, 53),       # N > 32: two-pass row kernel
+    ("softmax_cols_9000x3x1", (9000, 3, 1), 1, 54),       # M > 8192: chunked column kernel
+    ("softmax_vec_1000", (1000,), 1, 55),
+]
 
-def main(which=("dense", "backward", "windowed", "circulant")):
+
+def main(which=("dense", "backward", "windowed", "circulant", "softmax")):
+    if "softmax" in which:
+        for name, shape, dims, seed in SOFTMAX:
+            rng = np.random.default_rng(seed)
+            S = gen(rng, shape) * 4.0
+            print(save(name, in_s=S, p=O.fused_softmax(S, dims), dims=np.int64(dims)))
     if "circulant" in which:
         for name, N, d, dv, B, W, seed in CIRCULANT:
             rng = np.random.default_rng(seed)
@@ -150,4 +164,4 @@ def main(which=("dense", "backward", "windowed", "circulant")):
 
 if __name__ == "__main__":
     import sys
-    main(tuple(sys.argv[1:]) or ("dense", "backward", "windowed", "circulant"))
+    main(tuple(sys.argv[1:]) or ("dense", "backward", "windowed", "circulant", "softmax"))

@@ -27,7 +27,8 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("fa_dense_fwd", "fa_dense_bwd", "fa_dense_bwd_workspace", "fa_windowed_fwd",
               "fa_windowed_fwd_workspace", "fa_windowed_bwd", "fa_windowed_workspace",
-              "fa_circulant_fwd", "fa_last_error", "fa_abi_version", "fa_max_head_dim"):
+              "fa_circulant_fwd", "fa_softmax", "fa_softmax_workspace",
+              "fa_last_error", "fa_abi_version", "fa_max_head_dim"):
         assert f in fns
 
 
@@ -83,6 +84,15 @@ def test_invalid_arguments_return_status_and_message():
     assert rc == fa_hip.FA_ERR_UNSUPPORTED and b"head dimension" in L.fa_last_error()
     rc = L.fa_circulant_fwd(1, P, None, P, P, P, P, 64, 32, 32, 1, 7, 0.0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"null" in L.fa_last_error()
+    # softmax: dims, sizes and the long-column workspace are checked before any launch
+    rc = L.fa_softmax(1, P, P, 8, 8, 1, 3, None, 0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"dims" in L.fa_last_error()
+    rc = L.fa_softmax(1, P, P, 0, 8, 1, 1, None, 0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"DimensionMismatch" in L.fa_last_error()
+    assert L.fa_softmax_workspace(8192, 4, 1, 1) == 0 and L.fa_softmax_workspace(8193, 4, 1, 1) > 0
+    assert L.fa_softmax_workspace(100000, 4, 1, 2) == 0
+    rc = L.fa_softmax(1, P, P, 100000, 4, 1, 1, None, 0, None)
+    assert rc == fa_hip.FA_ERR_WORKSPACE
     # backward: workspace check happens before any launch
     need = L.fa_dense_bwd_workspace(1, 128, 128, 64, 64, 2)
     if need > 0:

@@ -231,3 +231,27 @@ def test_golden_circulant_reproduces(path):
     Oo, l, m = O.circulant_fa3(g["q"], g["k"], g["v"], W)
     assert np.allclose(Oo, g["o"], atol=1e-6)
     assert np.allclose(l, g["l"], rtol=1e-12) and np.allclose(m, g["m"], rtol=1e-12, atol=1e-12)
+
+
+# --- fused softmax (src/fused_softmax.jl:1-41) ---
+@pytest.mark.parametrize("shape,dims", [((7,), 1), ((6, 9), 1), ((6, 9), 2), ((5, 4, 3), 1), ((5, 4, 3), 2)])
+def test_fused_softmax_matches_torch(shape, dims):
+    rng = np.random.default_rng(sum(shape) + dims)
+    S = rng.standard_normal(shape) * 3
+    ref = torch.softmax(torch.tensor(S), dim=dims - 1).numpy()
+    assert np.allclose(O.fused_softmax(S, dims), ref, atol=1e-14)
+
+
+def test_fused_softmax_special_values():
+    """s .- maximum(s): an all -Inf column is NaN (-Inf - -Inf); -Inf entries
+    elsewhere give 0; a +Inf entry makes the vector NaN (Inf - Inf)."""
+    S = np.array([[-np.inf, 0.0, 1.0], [-np.inf, -np.inf, np.inf]]).T     # (3, 2) columns
+    P = O.fused_softmax(S, 1)
+    assert np.isnan(P[:, 1]).all()
+    assert P[0, 0] == 0.0 and np.isclose(P[:, 0].sum(), 1.0)
+
+
+@pytest.mark.parametrize("path", golden_files("softmax_"))
+def test_golden_softmax_reproduces(path):
+    g = load_golden(path)
+    assert np.allclose(O.fused_softmax(g["s"], int(g["dims"])), g["p"], atol=1e-7)
