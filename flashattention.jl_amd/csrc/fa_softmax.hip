@@ -15,7 +15,12 @@
 //    partials and writes (two reads, one write);
 //  * sm_rows: dims = 2, one thread per row i (lanes over consecutive i, so every
 //    access is coalesced across the wave), online (max, Σexp) over j, then a
-//    second pass that writes; rows of ≤ 32 elements stay in registers.
+//    second pass that writes; rows of ≤ 32 elements stay in registers;
+//  * sm_cols_reg_v / sm_rows_v: the same with 16-byte accesses whenever M is a
+//    multiple of 8 (bf16/fp16) or 4 (fp32) and S, P are 16-B aligned: a thread
+//    owns that many consecutive elements of a column, resp. consecutive rows
+//    (rows: the 4 waves of a workgroup split the columns and merge (max, Σexp)
+//    through LDS, so there are ≥ 8 workgroups per 4096 rows).
 #include <type_traits>
 
 #include "fa_common.h"
@@ -141,6 +146,130 @@ __global__ __launch_bounds__(kSmThreads) void sm_rows(const T* S, T* P, int64_t 
     }
 }
 
+// ---- 16-byte vectorised forms (M % VEC == 0, 16-B aligned S and P) ----
+template <class T> struct SmVec { static constexpr int n = 16 / (int)sizeof(T); };
+
+template <class T>
+__device__ __forceinline__ void unpack16(const u32x4 raw, float* f) {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // copy the lane out first: __builtin_bit_cast of an ext-vector element
+            // expression reads element 0 for every k (observed with hipcc, ROCm 7.2)
+            const unsigned w = raw[k];
+            f[k] = __builtin_bit_cast(float, w);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned w = raw[k];
+            f[2 * k] = (float)__builtin_bit_cast(T, (unsigned short)(w & 0xFFFFu));
+            f[2 * k + 1] = (float)__builtin_bit_cast(T, (unsigned short)(w >> 16));
+        }
+    }
+}
+
+template <class T>
+__device__ __forceinline__ u32x4 pack16(const float* f) {
+    u32x4 raw;
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) raw[k] = __builtin_bit_cast(unsigned, f[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned lo = __builtin_bit_cast(unsigned short, (T)f[2 * k]);
+            const unsigned hi = __builtin_bit_cast(unsigned short, (T)f[2 * k + 1]);
+            raw[k] = lo | (hi << 16);
+        }
+    }
+    return raw;
+}
+
+// dims = 1, column of M <= 8192 elements (M % VEC == 0) in registers as 16-B vectors
+template <class T>
+__global__ __launch_bounds__(kSmThreads) void sm_cols_reg_v(const T* S, T* P, int M) {
+    constexpr int VEC = SmVec<T>::n, NV = kSmEPT / VEC;   // vectors per thread
+    const int nvec = M / VEC;
+    const u32x4* Sv = (const u32x4*)(S + (int64_t)blockIdx.x * M);
+    u32x4* Pv = (u32x4*)(P + (int64_t)blockIdx.x * M);
+    float x[NV][VEC];
+    float m = kNegInf;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+        const int v = e * kSmThreads + threadIdx.x;
+        if (v < nvec) {
+            unpack16<T>(Sv[v], x[e]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) x[e][k] = kNegInf;
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) m = fmaxf(m, x[e][k]);
+    }
+    float l = 0.f;
+    if (m != kNegInf) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) l += __expf(x[e][k] - m);
+    }
+    block_ml(m, l);
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int e = 0; e < NV; ++e) {
+        const int v = e * kSmThreads + threadIdx.x;
+        if (v < nvec) {
+            float y[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) y[k] = __expf(x[e][k] - m) * inv;
+            Pv[v] = pack16<T>(y);
+        }
+    }
+}
+
+// dims = 2 with 16-B accesses (M % VEC == 0): a workgroup owns 64·VEC consecutive
+// rows (each lane VEC of them); its 4 waves split the N columns (j ≡ wave mod 4),
+// merge their (max, Σexp) partials through LDS, then each writes its columns.
+template <class T>
+__global__ __launch_bounds__(kSmThreads) void sm_rows_v(const T* S, T* P, int64_t M, int N) {
+    constexpr int VEC = SmVec<T>::n, NWV = kSmThreads / 64;
+    __shared__ float pm[NWV][64 * VEC], pl[NWV][64 * VEC];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t i0 = ((int64_t)blockIdx.x * 64 + lane) * VEC;
+    const bool act = i0 < M;
+    const int64_t base = (int64_t)blockIdx.y * M * N + i0;
+    float m[VEC], l[VEC], f[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) { m[k] = kNegInf; l[k] = 0.f; }
+    if (act) {
+        for (int j = wave; j < N; j += NWV) {
+            unpack16<T>(*(const u32x4*)(S + base + (int64_t)j * M), f);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) ml_merge(m[k], l[k], f[k], 1.0f);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) { pm[wave][lane * VEC + k] = m[k]; pl[wave][lane * VEC + k] = l[k]; }
+    __syncthreads();
+    float inv[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        float mm = pm[0][lane * VEC + k], ll = pl[0][lane * VEC + k];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) ml_merge(mm, ll, pm[w][lane * VEC + k], pl[w][lane * VEC + k]);
+        m[k] = mm;
+        inv[k] = 1.0f / ll;
+    }
+    if (!act) return;
+    for (int j = wave; j < N; j += NWV) {
+        unpack16<T>(*(const u32x4*)(S + base + (int64_t)j * M), f);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) f[k] = __expf(f[k] - m[k]) * inv[k];
+        *(u32x4*)(P + base + (int64_t)j * M) = pack16<T>(f);
+    }
+}
+
 size_t softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims) {
     if (dims != 1 || M <= kSmChunk) return 0;
     const int64_t nchunk = (M + kSmChunk - 1) / kSmChunk;
@@ -151,9 +280,13 @@ template <class T>
 static void launch_sm_typed(const SoftmaxArgs& a, hipStream_t s) {
     const T* S = (const T*)a.S;
     T* P = (T*)a.P;
+    constexpr int VEC = SmVec<T>::n;
+    const bool vec = a.M % VEC == 0 && ((uintptr_t)a.S & 15u) == 0 && ((uintptr_t)a.P & 15u) == 0;
     if (a.dims == 1) {
         const int64_t cols = a.N * a.batch;
-        if (a.M <= kSmChunk) {
+        if (a.M <= kSmChunk && vec) {
+            hipLaunchKernelGGL((sm_cols_reg_v<T>), dim3((unsigned)cols), dim3(kSmThreads), 0, s, S, P, (int)a.M);
+        } else if (a.M <= kSmChunk) {
             hipLaunchKernelGGL((sm_cols_reg<T>), dim3((unsigned)cols), dim3(kSmThreads), 0, s, S, P, (int)a.M);
         } else {
             const int nchunk = (int)((a.M + kSmChunk - 1) / kSmChunk);
@@ -162,6 +295,9 @@ static void launch_sm_typed(const SoftmaxArgs& a, hipStream_t s) {
             hipLaunchKernelGGL((sm_cols_part<T>), g, dim3(kSmThreads), 0, s, S, part, a.M, nchunk);
             hipLaunchKernelGGL((sm_cols_norm<T>), g, dim3(kSmThreads), 0, s, S, P, (const float2*)part, a.M, nchunk);
         }
+    } else if (vec && a.N > 32) {
+        const dim3 g((unsigned)((a.M / VEC + 63) / 64), (unsigned)a.batch);
+        hipLaunchKernelGGL((sm_rows_v<T>), g, dim3(kSmThreads), 0, s, S, P, a.M, (int)a.N);
     } else {
         const dim3 g((unsigned)((a.M + kSmThreads - 1) / kSmThreads), (unsigned)a.batch);
         if (a.N <= 32)

@@ -130,3 +130,20 @@ function circulant_fa(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::I
     m = similar(Q, Float32, N, 1, B)
     return circulant_fa!(O, l, m, Q, K, V, W)
 end
+
+# fused_softmax!(P, S; dims) — replaces src/fused_softmax.jl:10-15 (and the CUDA
+# versions src/cuda/fused_softmax.jl) for device arrays; P may be S
+function fused_softmax!(P::ROCArray{T,3}, S::ROCArray{T,3}; dims=1) where {T}
+    dims in (1, 2) || throw(ArgumentError("only softmax in dims 1 or 2 supported"))
+    size(P) == size(S) || throw(DimensionMismatch("P and S must have the same size"))
+    M, N, B = size(S)
+    nws = ccall((:fa_softmax_workspace, libfa_hip), Csize_t, (Int64, Int64, Int64, Cint), M, N, B, dims)
+    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    fa_check(ccall((:fa_softmax, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Int64, Cint, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                   fa_dtype(T), S, P, M, N, B, dims, ws, nws, stream_ptr()))
+    return P
+end
+fused_softmax!(P::ROCArray{T,2}, S::ROCArray{T,2}; dims=1) where {T} =
+    (fused_softmax!(reshape(P, size(P)..., 1), reshape(S, size(S)..., 1); dims=dims); P)
+fused_softmax(S::ROCArray; dims=1) = fused_softmax!(similar(S), S; dims=dims)
