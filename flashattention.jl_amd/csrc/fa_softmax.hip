@@ -308,8 +308,9 @@ static void launch_sm_typed(const SoftmaxArgs& a, hipStream_t s) {
 }
 
 int launch_softmax(const SoftmaxArgs& a, hipStream_t s, const char** why) {
-    if (a.N > INT32_MAX || a.batch > 65535 || (a.dims == 1 && a.N * a.batch * ((a.M + kSmChunk - 1) / kSmChunk) > UINT32_MAX) ||
-        (a.dims == 2 && (a.M + kSmThreads - 1) / kSmThreads > UINT32_MAX)) {
+    // grid limits: x <= 2^31 - 1 blocks; dims = 2 puts the batch on grid.y (<= 65535)
+    if (a.N > INT32_MAX || (a.dims == 1 && a.N * a.batch * ((a.M + kSmChunk - 1) / kSmChunk) > INT32_MAX) ||
+        (a.dims == 2 && (a.batch > 65535 || (a.M + kSmThreads - 1) / kSmThreads > INT32_MAX))) {
         *why = "extent exceeds the launch grid";
         return FA_ERR_UNSUPPORTED;
     }

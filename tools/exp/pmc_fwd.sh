@@ -9,6 +9,6 @@ timeout -k 10 120 rocprofv3 --list-avail > $OUT/avail.txt 2>&1 || true
 i=0
 for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 tools/exp/fwd_run.py $VARS > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 ${PMC_SCRIPT:-tools/exp/fwd_run.py} $VARS > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
 done
 echo done
