@@ -103,6 +103,32 @@ function windowed_fa(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,N}, windo
     return y, l, m
 end
 
+# windowed_fa_backward(q, k, v, y, dy, l, m, ws; stride, pad) — the chain rule of
+# windowed_fa (SURVEY §8f row 1; the reference README claims it, no code exists)
+function windowed_fa_backward(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,N},
+                              y::ROCArray{T,N}, dy::ROCArray{T,N},
+                              l::ROCArray{Float32}, m::ROCArray{Float32}, windowsize;
+                              stride=windowsize, pad=(windowsize - 1) ÷ 2) where {T,N}
+    nsp = N - 2
+    spatial = Int64[size(q, i) for i in 1:nsp]
+    d, dv, B = size(q, N - 1), size(v, N - 1), size(q, N)
+    dq, dk, dv_ = similar(q), similar(k), similar(v)
+    nws = ccall((:fa_windowed_workspace, libfa_hip), Csize_t,
+                (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),
+                fa_dtype(T), nsp, spatial, d, dv, B, windowsize, stride, pad)
+    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    fa_check(ccall((:fa_windowed_bwd, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                    Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64,
+                    Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                   fa_dtype(T), q, k, v, y, dy, l, m, dq, dk, dv_, nsp, spatial, d, dv, B,
+                   windowsize, stride, pad, 0f0, ws, nws, stream_ptr()))
+    return dq, dk, dv_
+end
+
+fa_abi_version() = ccall((:fa_abi_version, libfa_hip), Cint, ())
+fa_max_head_dim() = ccall((:fa_max_head_dim, libfa_hip), Cint, ())
+
 # block_fa — src/windowed.jl:1
 block_fa(q::ROCArray, k::ROCArray, v::ROCArray, windowsize; pad=0) =
     windowed_fa(q, k, v, windowsize; stride=windowsize, pad=pad)
