@@ -78,7 +78,7 @@ int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
 // wave} = {4,1}, {8,1}, {4,2}, {8,2}.
 int fa_debug_set_fwd_variant(int v) {
     const int old = fa::g_fwd_variant;
-    if (v == 0 || (v >= 4 && v <= 8)) fa::g_fwd_variant = v;
+    if (v == 0 || (v >= 4 && v <= 7)) fa::g_fwd_variant = v;
     return old;
 }
 

@@ -693,261 +693,6 @@ template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
 
 // --------------------------------------------------------------------------
-// Software-pipelined forward (bf16 / fp16): 8 waves x 32 query rows.  Within
-// one wave, iteration j overlaps
-//     exp / row sum of S(j)   with   Sᵀ(j+1) = K(j+1)·Qᵀ   (MFMA)
-//     row max of S(j+1)       with   Oᵀ += Vᵀ(j)·Pᵀ(j)      (MFMA)
-// so the vector work of the online softmax runs beside the matrix work of the
-// neighbouring tile instead of in a VALU-only stretch (both waves of a SIMD
-// reach the barrier in lockstep, so without this the matrix pipe idles while
-// they exponentiate).  K(j+1) must be resident during iteration j: a 3-slot
-// LDS ring, tile j+2 stored and tile j+3 loaded in iteration j, one barrier
-// per tile.  The loop is unrolled x2 so S(j) / S(j+1) swap roles without
-// register copies; the last two tiles (the only ones that can be ragged or
-// lack a successor) are peeled.
-// --------------------------------------------------------------------------
-template <class T, int D, int DV>
-__global__ __launch_bounds__(512, 1) void dense_fwd_swp(FwdParams p) {
-    typedef typename Frag8<T>::type F8;
-    typedef typename Frag8<T>::half F4;
-    constexpr int NTH = 512, BM = 256, BN = 64, NKB = 2;
-    constexpr int KROW = BN * 2, VROW = BN * 2 + 16;
-    constexpr int KBYTES = D * KROW, VBYTES = DV * VROW, STAGE = KBYTES + VBYTES;
-    constexpr int CPR = BN / 8;
-    constexpr int KTOT = D * CPR, VTOT = DV * CPR;
-    constexpr int KCH = (KTOT + NTH - 1) / NTH, VCH = (VTOT + NTH - 1) / NTH;
-    static_assert(KTOT % NTH == 0 || KTOT < NTH, "tile split");
-    static_assert(VTOT % NTH == 0 || VTOT < NTH, "tile split");
-    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE + 16];
-    auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
-    auto opaque = [](int v) { asm volatile("" : "+v"(v)); return v; };
-
-    const int lid = xcd_remap(blockIdx.x, p.total_wg);
-    const int b = lid / p.nqb;
-    const int qb = lid - b * p.nqb;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
-    const auto qrs = slab_rsrc((const T*)p.Q + (int64_t)b * N * d, (uint32_t)(N * d * (int)sizeof(T)));
-    const auto krs = slab_rsrc((const T*)p.K + (int64_t)b * Nk * d, (uint32_t)(Nk * d * (int)sizeof(T)));
-    const auto vrs = slab_rsrc((const T*)p.V + (int64_t)b * Nk * dv, (uint32_t)(Nk * dv * (int)sizeof(T)));
-
-    const int qi = qb * BM + wave * 32 + r;
-    F8 qf[D / 16];
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-            qf[s][e] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(qrs, ((16 * s + 8 * h + e) * N + qi) * 2, 0, 0));
-
-    const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-    int koff[NKB];
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-        koff[kb] = (8 * h + qq) * KROW + (((kb * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
-    const int voff = r * VROW + 16 * h;
-
-    const bool kact = KTOT >= NTH || tid < KTOT, vact = VTOT >= NTH || tid < VTOT;
-    int kgo[KCH], kso[KCH], vgo[VCH], vso[VCH];
-#pragma unroll
-    for (int it = 0; it < KCH; ++it) {
-        const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
-        kgo[it] = kact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
-        kso[it] = kact ? f * KROW + (((pc >> 1) ^ kswz(f)) * 32) + (pc & 1) * 16 : 3 * STAGE;
-    }
-#pragma unroll
-    for (int it = 0; it < VCH; ++it) {
-        const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
-        vgo[it] = vact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
-        vso[it] = vact ? KBYTES + f * VROW + pc * 16 : 3 * STAGE;
-    }
-
-    const float c = p.scale_log2;
-    const float thr_raw = kRescaleLog2 / c;
-    const int NT = (Nk + BN - 1) / BN;
-    const bool ragged = (Nk % BN) != 0;
-
-    u32x4 kreg[KCH], vreg[VCH];
-    auto gload = [&](int t) {        // tiles past the end read zeros (buffer bounds)
-        const int o = t * BN * 2;
-#pragma unroll
-        for (int it = 0; it < KCH; ++it) kreg[it] = __builtin_amdgcn_raw_buffer_load_b128(krs, kgo[it] + o, 0, 0);
-#pragma unroll
-        for (int it = 0; it < VCH; ++it) vreg[it] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vgo[it] + o, 0, 0);
-    };
-    auto lstore = [&](int t, int slot) {
-        if (ragged && t == NT - 1) {   // keys >= Nk: V rows must be 0 (0·garbage may be NaN)
-#pragma unroll
-            for (int it = 0; it < VCH; ++it) {
-                const int ch = tid + NTH * it;
-                if (t * BN + (ch % CPR) * 8 >= Nk) vreg[it] = u32x4{0u, 0u, 0u, 0u};
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < KCH; ++it)
-            *(u32x4*)(smem + opaque((KTOT >= NTH || kact) ? kso[it] + slot : 3 * STAGE)) = kreg[it];
-#pragma unroll
-        for (int it = 0; it < VCH; ++it)
-            *(u32x4*)(smem + opaque((VTOT >= NTH || vact) ? vso[it] + slot : 3 * STAGE)) = vreg[it];
-    };
-
-    f32x16 oacc[DV / 32];
-#pragma unroll
-    for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-        for (int x = 0; x < 16; ++x) oacc[cb][x] = 0.0f;
-    float m_used = kNegInf, m_true = kNegInf, l_run = 0.0f;
-
-    auto qk = [&](f32x16 (&sn)[NKB], int slot) {
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-            const char* kl = smem + opaque(koff[kb] + slot);
-#pragma unroll
-            for (int x = 0; x < 16; ++x) sn[kb][x] = 0.0f;
-#pragma unroll
-            for (int s = 0; s < D / 16; ++s) {
-                const char* a = kl + 16 * s * KROW;
-                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
-                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW));
-                sn[kb] = mfma32x32x16(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), qf[s], sn[kb]);
-            }
-        }
-    };
-    auto mask = [&](f32x16 (&sn)[NKB], int t) {
-        const int key0 = t * BN;
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
-                if (key0 + kt >= Nk) sn[kb][x] = kNegInf;
-            }
-    };
-    auto rowmax = [&](const f32x16 (&sn)[NKB]) {
-        float pm[4] = {sn[0][0], sn[0][1], sn[0][2], sn[0][3]};
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sn[kb][x]);
-        return swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
-    };
-    auto rescale = [&](float mt) {
-        m_true = fmaxf(m_true, mt);
-        if (__builtin_amdgcn_ballot_w64(mt > m_used + thr_raw) != 0) {
-            const float m_new = fmaxf(m_used, mt);
-            const float alpha = exp2_fast((m_used - m_new) * c);
-            l_run *= alpha;
-#pragma unroll
-            for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) oacc[cb][x] *= alpha;
-            m_used = m_new;
-        }
-    };
-    F8 pf[NKB][2];
-    auto expsum = [&](const f32x16 (&sc)[NKB]) {
-        const float mc = m_used * c;
-        float ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const float pv = exp2_fast(fmaf(sc[kb][x], c, -mc));
-                ps[x & 3] += pv;
-                pf[kb][x >> 3][x & 7] = (T)pv;
-            }
-        l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-    };
-    auto pv = [&](int slot) {
-        const char* vl = smem + opaque(voff + slot) + KBYTES;
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const F8 va = *(const F8*)(vl + cb * 32 * VROW + (kb * 32 + 16 * s) * 2);
-                    oacc[cb] = mfma32x32x16(va, pf[kb][s], oacc[cb]);
-                }
-    };
-
-    // slots (byte offsets) of tiles j, j+1, j+2
-    int s0 = 0, s1 = STAGE, s2 = 2 * STAGE;
-    auto rot = [&]() { const int t = s0; s0 = s1; s1 = s2; s2 = t; };
-
-    f32x16 sA[NKB], sB[NKB];
-    // prologue: tiles 0, 1 resident, tile 2 in flight; S(0) and its max
-    gload(0);
-    lstore(0, s0);
-    if (NT > 1) { gload(1); lstore(1, s1); }
-    gload(2);
-    __syncthreads();
-    qk(sA, s0);
-    if (ragged && NT == 1) mask(sA, 0);
-    float mt = rowmax(sA);
-
-    // steady state: iteration j (0 <= j <= NT-3) — QK(j+1) never masked,
-    // tile j+2 stored, tile j+3 loaded
-    auto steady = [&](f32x16 (&sc)[NKB], f32x16 (&sn)[NKB], int j) {
-        rescale(mt);
-        expsum(sc);
-        qk(sn, s1);
-        pv(s0);
-        mt = rowmax(sn);
-        lstore(j + 2, s2);
-        gload(j + 3);
-        __syncthreads();
-        rot();
-    };
-    int j = 0;
-    for (; j + 1 < NT - 2; j += 2) {
-        steady(sA, sB, j);
-        steady(sB, sA, j + 1);
-    }
-    if (j < NT - 2) {                        // odd count: one more, then S(j+1) lives in sB
-        steady(sA, sB, j);
-        ++j;
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) sA[kb] = sB[kb];
-    }
-    // j = NT-2: QK of the last (possibly ragged) tile
-    if (NT >= 2) {
-        rescale(mt);
-        expsum(sA);
-        qk(sB, s1);
-        if (ragged) mask(sB, NT - 1);
-        pv(s0);
-        mt = rowmax(sB);
-        rot();
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) sA[kb] = sB[kb];
-    }
-    // j = NT-1
-    rescale(mt);
-    expsum(sA);
-    pv(s0);
-
-    const float lt = swap_halves_sum(l_run);
-    if (qi < N) {
-        const float inv = 1.0f / lt;
-        T* Ob = (T*)p.O + (int64_t)b * N * dv;
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int cc = cb * 32 + acc_row(x, h);
-                if (cc < dv) Ob[(int64_t)cc * N + qi] = (T)(oacc[cb][x] * inv);
-            }
-        if (h == 0) {
-            p.m[(int64_t)b * N + qi] = m_true * p.scale;
-            p.l[(int64_t)b * N + qi] = lt * exp2_fast((m_used - m_true) * c);
-        }
-    }
-}
-
-// --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
 template <class T, int D>
@@ -971,17 +716,7 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
             case 128: hipLaunchKernelGGL((KER<T, D, 128>), g2, blk, 0, s, q); break;    \
             default: return hipErrorInvalidValue;                                       \
         }
-        if (v == 8) {
-            q.nqb = (q.N + 255) / 256;
-            q.total_wg = q.nqb * (int)(p.total_wg / p.nqb);
-            const dim3 g3((unsigned)q.total_wg);
-            switch (DVc) {
-                case 32: hipLaunchKernelGGL((dense_fwd_swp<T, D, 32>), g3, dim3(512), 0, s, q); break;
-                case 64: hipLaunchKernelGGL((dense_fwd_swp<T, D, 64>), g3, dim3(512), 0, s, q); break;
-                case 128: hipLaunchKernelGGL((dense_fwd_swp<T, D, 128>), g3, dim3(512), 0, s, q); break;
-                default: return hipErrorInvalidValue;
-            }
-        } else if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
+        if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
         else if (v == 5) { FA_LAUNCH_T(dense_fwd_w8b64) }
         else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
         else { FA_LAUNCH_T(dense_fwd_w8q2) }
