@@ -136,3 +136,19 @@ def test_backward_fast_matches_generic(fa, N, Nk, d, dv):
     torch.cuda.synchronize()
     for a, b, nm in zip(fast, gen, ("dQ", "dK", "dV")):
         assert_grad_close(_np(a), _np(b), "bfloat16", nm)
+
+
+@pytest.mark.parametrize("d,dv", [(48, 48), (80, 96), (96, 32), (16, 128)])
+def test_backward_head_dim_sweep(fa, d, dv):
+    """Head dims outside {32, 64, 128} take the generic backward; 32/64/128
+    combinations the fast one — both against the oracle."""
+    rng = np.random.default_rng(d + 7 * dv)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    q, k = bf(rng.standard_normal((192, d, 2))), bf(rng.standard_normal((256, d, 2)))
+    v, do = bf(rng.standard_normal((256, dv, 2))), bf(rng.standard_normal((192, dv, 2)))
+    dq, dk, dv_, Odev = run_bwd(fa, q, k, v, do, "bfloat16")
+    Oo, l, m = O.dense_fa3(q, k, v)
+    dqr, dkr, dvr = O.dense_fa_backward(q, k, v, Odev, do, l, m)
+    assert_grad_close(dq, dqr, "bfloat16", "dQ")
+    assert_grad_close(dk, dkr, "bfloat16", "dK")
+    assert_grad_close(dv_, dvr, "bfloat16", "dV")

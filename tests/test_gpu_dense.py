@@ -185,3 +185,37 @@ def test_config2_full_size_properties(fa):
 def test_config4_full_size_forward_properties(fa):
     """BASELINE configs[3] forward: (4,16,8192,128) bf16 → (8192, 128, 64)."""
     _full_size_properties(fa, 8192, 128, 64, torch.bfloat16, check_slabs=(5,))
+
+
+@pytest.mark.parametrize("d,dv", [(8, 8), (24, 40), (48, 48), (56, 72), (80, 80), (96, 64), (104, 120), (112, 112), (120, 24)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_head_dim_sweep_fast_path(fa, d, dv, dtype):
+    """Head dims that are not 32/64/128 run the fast kernels zero-padded to the next
+    class (aligned N, Nk: the fast path), for d != dv in both directions."""
+    rng = np.random.default_rng(d * 131 + dv)
+    rd = lambda a: torch.tensor(a).to(DT[dtype]).double().numpy()
+    q, k, v = rd(rng.standard_normal((256, d, 2))), rd(rng.standard_normal((320, d, 2))), rd(rng.standard_normal((320, dv, 2)))
+    y, l, m = fa.dense_fa(*(fa.jl_tensor(a, DT[dtype]) for a in (q, k, v)))
+    torch.cuda.synchronize()
+    yr, lr, mr = O.dense_fa3(q, k, v)
+    assert_close(_np(y), yr, dtype, "y")
+    assert_lm_close(_np(l), lr, dtype, "l")
+    assert_lm_close(_np(m), mr, dtype, "m")
+
+
+def test_long_single_slab(fa):
+    """One slab with N = Nk = 65536 (512 key tiles, 128 query blocks): the oracle
+    on the first and last query blocks (K, V over the whole sequence)."""
+    N, d = 65536, 64
+    g = torch.Generator(device="cuda").manual_seed(11)
+    Q, K, V = (fa.jl_empty((N, d, 1), torch.bfloat16) for _ in range(3))
+    for t in (Q, K, V):
+        t.copy_(torch.randn((N, d, 1), generator=g, device="cuda"))
+    y, l, m = fa.dense_fa(Q, K, V)
+    torch.cuda.synchronize()
+    Kh, Vh = _np(K), _np(V)
+    for r0 in (0, N - 128):
+        yr, lr, mr = O.dense_fa3(_np(Q[r0:r0 + 128]), Kh, Vh)
+        assert_close(_np(y[r0:r0 + 128]), yr, "bfloat16", f"y[{r0}]")
+        assert_lm_close(_np(l[r0:r0 + 128]), lr, "bfloat16", "l")
+        assert_lm_close(_np(m[r0:r0 + 128]), mr, "bfloat16", "m")
