@@ -168,24 +168,26 @@ __global__ __launch_bounds__(256, 2) void circ_fwd_tiled(CircParams P) {
         vso[it] = vact ? KBYTES + vf[it] * VROW + vpc[it] * 16 : 2 * STAGE;
     }
 
-    u32x4 kreg[KCH], vreg[VCH];
-    auto gload = [&](int t) {        // 8-key chunks never straddle N (k0 % 8 == 0, N % 8 == 0)
+    // two register sets: a tile's global loads are issued two iterations before
+    // its LDS store, so the (latency-bound) short band loop overlaps them
+    u32x4 kreg[2][KCH], vreg[2][VCH];
+    auto gload = [&](int t, int set) {   // 8-key chunks never straddle N (k0 % 8 == 0, N % 8 == 0)
 #pragma unroll
         for (int it = 0; it < KCH; ++it) {
             const int key = (k0 + t * BN + 8 * kpc[it]) % N;
-            kreg[it] = __builtin_amdgcn_raw_buffer_load_b128(krs, kact ? (kf[it] * N + key) * 2 : 0x7FFFFFF0, 0, 0);
+            kreg[set][it] = __builtin_amdgcn_raw_buffer_load_b128(krs, kact ? (kf[it] * N + key) * 2 : 0x7FFFFFF0, 0, 0);
         }
 #pragma unroll
         for (int it = 0; it < VCH; ++it) {
             const int key = (k0 + t * BN + 8 * vpc[it]) % N;
-            vreg[it] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vact ? (vf[it] * N + key) * 2 : 0x7FFFFFF0, 0, 0);
+            vreg[set][it] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vact ? (vf[it] * N + key) * 2 : 0x7FFFFFF0, 0, 0);
         }
     };
-    auto lstore = [&](char* buf) {
+    auto lstore = [&](char* buf, int set) {
 #pragma unroll
-        for (int it = 0; it < KCH; ++it) *(u32x4*)((kact ? buf : smem) + kso[it]) = kreg[it];
+        for (int it = 0; it < KCH; ++it) *(u32x4*)((kact ? buf : smem) + kso[it]) = kreg[set][it];
 #pragma unroll
-        for (int it = 0; it < VCH; ++it) *(u32x4*)((vact ? buf : smem) + vso[it]) = vreg[it];
+        for (int it = 0; it < VCH; ++it) *(u32x4*)((vact ? buf : smem) + vso[it]) = vreg[set][it];
     };
 
     f32x16 oacc[DV / 32];
@@ -267,18 +269,25 @@ __global__ __launch_bounds__(256, 2) void circ_fwd_tiled(CircParams P) {
 
     char* const buf0 = smem;
     char* const buf1 = smem + STAGE;
-    gload(0);
-    lstore(buf0);
+    // tile t: registers set t % 2 (loaded at iteration t-2), LDS buffer t % 2
+    gload(0, 0);
+    if (NT > 1) gload(1, 1);
+    lstore(buf0, 0);
+    if (NT > 2) gload(2, 0);
     __syncthreads();
     for (int t = 0; t < NT; t += 2) {
-        gload(min(t + 1, NT - 1));
         if (t >= tlo && t <= thi) compute(buf0, t);
-        lstore(buf1);
+        if (t + 1 < NT) {
+            lstore(buf1, 1);
+            if (t + 3 < NT) gload(t + 3, 1);
+        }
         __syncthreads();
         if (t + 1 < NT) {
-            gload(min(t + 2, NT - 1));
             if (t + 1 >= tlo && t + 1 <= thi) compute(buf1, t + 1);
-            lstore(buf0);
+            if (t + 2 < NT) {
+                lstore(buf0, 0);
+                if (t + 4 < NT) gload(t + 4, 0);
+            }
             __syncthreads();
         }
     }
