@@ -92,7 +92,7 @@ int fa_debug_set_bwd_generic(int v) {
 // Not part of the public header: 1 forces the composed windowed forward.
 int fa_debug_set_win_composed(int v) {
     const int old = fa::g_win_force_composed;
-    fa::g_win_force_composed = v != 0;
+    fa::g_win_force_composed = (v == 1 || v == 2) ? v : 0;
     return old;
 }
 

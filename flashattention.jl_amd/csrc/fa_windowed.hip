@@ -300,12 +300,211 @@ static bool fully_covered(const WindowGeom& g) {
     return true;
 }
 
-int g_win_force_composed = 0;   // benchmark knob
+// --------------------------------------------------------------------------
+// Row-staged single-pass windowed forward (2-D, stride >= ws, ws <= 8,
+// bf16/fp16, d, dv <= 64, image width % 8 == 0).  The register-gather kernel
+// above is texture-addresser bound (2-byte gathers across 64 feature planes:
+// profiles/r01_windowed_ta_counters.txt).  Here a workgroup owns 4 adjacent
+// windows of one window row; lanes load IMAGE-ALIGNED 16-byte chunks along
+// x (never straddling a row, no shifts, no negative offsets) and scatter the
+// pixels into per-window token slots in LDS (slot = 8·ty + tx, the dense
+// forward's swizzled [feature][slot] images).  Features stream in chunks (16
+// for q, k — Sᵀ accumulates in registers across chunks; 32 for v), so the LDS
+// footprint is one chunk.  Out-of-image pixels and padding slots stay zero
+// (zero-filled image): the reference's zero padding.
+// --------------------------------------------------------------------------
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, const T* __restrict__ k,
+                                                   const T* __restrict__ v, T* __restrict__ out,
+                                                   float* __restrict__ lo, float* __restrict__ mo,
+                                                   WinDev g, int d, int dv, int batch, int ngx,
+                                                   float scale, float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int NWIN = 4, NTH = 256;
+    constexpr int FQ = 16, FV = 32;                            // feature chunk: q/k, v
+    constexpr int KROW = 128, VROW = 144;
+    constexpr int QKIMG = FQ * KROW;                           // one window, one tensor, one q/k chunk
+    constexpr int VIMG = FV * VROW;
+    constexpr int REGION = (2 * NWIN * QKIMG > NWIN * VIMG) ? 2 * NWIN * QKIMG : NWIN * VIMG;
+    __shared__ __attribute__((aligned(16))) char smem[REGION];
+    auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
+
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
+    int bid = blockIdx.x;
+    const int gx = bid % ngx; bid /= ngx;
+    const int wy = bid % g.O[1];
+    const int b = bid / g.O[1];
+    const int wx0 = gx * NWIN;
+    const int nwin = min(NWIN, g.O[0] - wx0);
+    const int xs = wx0 * st - g.pad;                           // x of window 0, token 0
+    const int xe = (wx0 + nwin - 1) * st - g.pad + ws;         // one past the last window's pixels
+    const int y0 = wy * st - g.pad;
+    const int c_lo = max(xs, 0) >> 3, c_hi = (min(xe, W_) + 7) >> 3;   // image-aligned 8-pixel chunks
+    const int ncx = c_hi - c_lo;
+    const int ylo = max(y0, 0), yhi = min(y0 + ws, H_);
+    const int nrow = max(yhi - ylo, 0);
+
+    // zero the staging region, then scatter nf features (from feature f0) of
+    // tensor src into image base + wl·imgbytes with the given row layout
+    auto zero_region = [&]() {
+        for (int o = tid * 16; o < REGION; o += NTH * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+    };
+    auto stage = [&](const T* src, int C, int f0, int nf, int base, int imgbytes, bool vlayout) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (int64_t)b * C * P_), (short)0, C * P_ * 2, 0x00020000);
+        const int items = nf * nrow * ncx;
+        for (int it = tid; it < items; it += NTH) {
+            const int cx = it % ncx;
+            const int rest = it / ncx;
+            const int yy = rest % nrow, fl = rest / nrow;
+            const int f = f0 + fl, y = ylo + yy, x8 = (c_lo + cx) * 8;
+            u32x4 val = u32x4{0u, 0u, 0u, 0u};
+            if (f < C) val = __builtin_amdgcn_raw_buffer_load_b128(rs, (f * P_ + y * W_ + x8) * 2, 0, 0);
+            const int ty = y - y0;
+            // (window, token column) of the chunk's first pixel; consecutive pixels
+            // then advance incrementally (tx < 0: left of window 0)
+            const int rel = x8 - xs;
+            int wl = rel >= 0 ? rel / st : 0;
+            int tx = rel >= 0 ? rel - wl * st : rel;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (tx >= 0 && tx < ws && wl < nwin) {
+                    const unsigned wd = val[e >> 1];
+                    const unsigned short px = (unsigned short)((e & 1) ? (wd >> 16) : (wd & 0xFFFFu));
+                    const int slot = ty * 8 + tx;
+                    const int o = vlayout ? fl * VROW + slot * 2
+                                          : fl * KROW + (((slot >> 4) ^ kswz(fl)) * 32) + (slot & 15) * 2;
+                    *(unsigned short*)(smem + base + wl * imgbytes + o) = px;
+                }
+                if (++tx == st) { tx = 0; ++wl; }
+            }
+        }
+    };
+
+    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    f32x16 sa[2][2];                                           // [key block][query block]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sa[kb][qb][x] = 0.0f;
+
+    // ---- Sᵀ = K·Qᵀ over feature chunks of 16 ----
+    for (int f0 = 0; f0 < D; f0 += FQ) {
+        zero_region();
+        __syncthreads();
+        stage(q, d, f0, FQ, 0, QKIMG, false);
+        stage(k, d, f0, FQ, NWIN * QKIMG, QKIMG, false);
+        __syncthreads();
+        if (wave < nwin) {
+            const char* qimg = smem + wave * QKIMG;
+            const char* kimg = smem + NWIN * QKIMG + wave * QKIMG;
+            F8 kf[2], qf[2];
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk) {
+                const int o = (8 * h + qq) * KROW + (((blk * 2 + kh) ^ kswz(qq)) * 32);
+                kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(kimg + o + 8 * sig)),
+                                                  __builtin_bit_cast(F4, ds_read_tr16(kimg + o + 8 * sig + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+                qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(qimg + o + 8 * pp)),
+                                                  __builtin_bit_cast(F4, ds_read_tr16(qimg + o + 8 * pp + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) sa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], sa[kb][qb]);
+        }
+        __syncthreads();
+    }
+
+    // ---- exact softmax per query (keys: the window's ws x ws real slots) ----
+    F8 pf[2][2][2];                                            // [query block][key block][half]
+    float mt[2], lt[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+                if ((kt & 7) >= ws || (kt >> 3) >= ws) sa[kb][qb][x] = kNegInf;
+            }
+        float pm[4] = {sa[0][qb][0], sa[0][qb][1], sa[0][qb][2], sa[0][qb][3]};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sa[kb][qb][x]);
+        mt[qb] = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+        const float mc = mt[qb] * scale_log2;
+        float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = exp2_fast(fmaf(sa[kb][qb][x], scale_log2, -mc));
+                ps[x & 3] += pr;
+                pf[qb][kb][x >> 3][x & 7] = (T)pr;
+            }
+        lt[qb] = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+    }
+
+    // ---- Oᵀ = Vᵀ·Pᵀ over feature chunks of 32, stored straight to the pixels ----
+    const int wx = wx0 + wave;
+    const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+    for (int c0 = 0; c0 < DV; c0 += FV) {
+        zero_region();
+        __syncthreads();
+        stage(v, dv, c0, FV, 0, VIMG, true);
+        __syncthreads();
+        if (wave < nwin) {
+            const char* vimg = smem + wave * VIMG + r * VROW + 16 * h;
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                f32x16 oa;
+#pragma unroll
+                for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+                        oa = mfma32x32x16(*(const F8*)(vimg + (kb * 32 + 16 * s2) * 2), pf[qb][kb][s2], oa);
+                const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
+                const int px = wx * st - g.pad + qtx, py = y0 + qty;
+                if (qtx < ws && qty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+                    const float inv = 1.0f / lt[qb];
+                    T* yb = out + (int64_t)b * dv * P_ + (int64_t)py * W_ + px;
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) {
+                        const int cc = c0 + acc_row(x, h);
+                        if (cc < dv) yb[(int64_t)cc * P_] = (T)(oa[x] * inv);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (wave < nwin && h == 0) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
+            if (qtx < ws && qty < ws) {
+                const int64_t li = qty * ws + qtx + (int64_t)g.T * wid;
+                mo[li] = mt[qb] * scale;
+                lo[li] = lt[qb];
+            }
+        }
+    }
+}
+
+int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
 static bool fused_ok(int dtype, const WindowGeom& g, int64_t d, int64_t dv) {
-    return !g_win_force_composed && dtype != FA_DTYPE_F32 && g.T <= 64 && d <= 64 && dv <= 64 &&
+    return g_win_force_composed != 1 && dtype != FA_DTYPE_F32 && g.T <= 64 && d <= 64 && dv <= 64 &&
            g.P * (d > dv ? d : dv) * 2 < INT32_MAX;
 }
 
@@ -321,9 +520,36 @@ static hipError_t launch_fused_dd(const WindowedArgs& a, const WinDev& g, void* 
 #undef FA_FUSED
     return hipGetLastError();
 }
+// Row-staged kernel: 2-D, non-overlapping (direct store), ws <= 8, width % 8 == 0,
+// 16-B aligned tensors (image-aligned 16-B row chunks).  Below ~1024 windows its
+// six serial feature-chunk phases are exposed (B = 1 of configs[2]: 38 vs 31 µs)
+// and the register-gather kernel is faster.
+static bool rows_ok(const WindowedArgs& a) {
+    return g_win_force_composed != 2 && a.g.L * a.batch >= 1024 && a.g.nsp == 2 &&
+           a.g.stride >= a.g.ws && a.g.ws <= 8 &&
+           a.g.S[0] % 8 == 0 && ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 &&
+           ((uintptr_t)a.v & 15u) == 0;
+}
+
+template <class T, int D, int DV>
+static hipError_t launch_rows_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
+    const int ngx = (int)((a.g.O[0] + 3) / 4);
+    const int64_t nwg = (int64_t)ngx * a.g.O[1] * a.batch;
+    hipLaunchKernelGGL((win_rows<T, D, DV>), dim3((unsigned)nwg), dim3(256), 0, s, (const T*)a.q, (const T*)a.k,
+                       (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, (int)a.batch, ngx, a.scale,
+                       a.scale * kLog2e);
+    return hipGetLastError();
+}
+
 template <class T>
 static hipError_t launch_fused(const WindowedArgs& a, const WinDev& g, void* out, bool direct, hipStream_t s) {
     const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
+    if (direct && out == a.y && rows_ok(a)) {
+        if (Dc == 32 && DVc == 32) return launch_rows_dd<T, 32, 32>(a, g, s);
+        if (Dc == 32) return launch_rows_dd<T, 32, 64>(a, g, s);
+        if (DVc == 32) return launch_rows_dd<T, 64, 32>(a, g, s);
+        return launch_rows_dd<T, 64, 64>(a, g, s);
+    }
     if (Dc == 32 && DVc == 32) return launch_fused_dd<T, 32, 32>(a, g, out, direct, s);
     if (Dc == 32) return launch_fused_dd<T, 32, 64>(a, g, out, direct, s);
     if (DVc == 32) return launch_fused_dd<T, 64, 32>(a, g, out, direct, s);
