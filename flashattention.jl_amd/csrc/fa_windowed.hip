@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, cons
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
     constexpr int NWIN = 4, NTH = 256;
-    constexpr int FQ = 16, FV = 32;                            // feature chunk: q/k, v
+    constexpr int FQ = D < 32 ? D : 32, FV = 32;              // feature chunk: q/k, v
     constexpr int KROW = 128, VROW = 144;
     constexpr int QKIMG = FQ * KROW;                           // one window, one tensor, one q/k chunk
     constexpr int VIMG = FV * VROW;
@@ -393,29 +393,34 @@ __global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, cons
 #pragma unroll
             for (int x = 0; x < 16; ++x) sa[kb][qb][x] = 0.0f;
 
-    // ---- Sᵀ = K·Qᵀ over feature chunks of 16 ----
+    // ---- Sᵀ = K·Qᵀ over feature chunks.  Every chunk writes the same slot
+    //      positions (pixel validity does not depend on the feature), so the
+    //      padding slots stay zero after one zero-fill per layout. ----
+    zero_region();
+    __syncthreads();
     for (int f0 = 0; f0 < D; f0 += FQ) {
-        zero_region();
-        __syncthreads();
         stage(q, d, f0, FQ, 0, QKIMG, false);
         stage(k, d, f0, FQ, NWIN * QKIMG, QKIMG, false);
         __syncthreads();
         if (wave < nwin) {
             const char* qimg = smem + wave * QKIMG;
             const char* kimg = smem + NWIN * QKIMG + wave * QKIMG;
-            F8 kf[2], qf[2];
 #pragma unroll
-            for (int blk = 0; blk < 2; ++blk) {
-                const int o = (8 * h + qq) * KROW + (((blk * 2 + kh) ^ kswz(qq)) * 32);
-                kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(kimg + o + 8 * sig)),
-                                                  __builtin_bit_cast(F4, ds_read_tr16(kimg + o + 8 * sig + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
-                qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(qimg + o + 8 * pp)),
-                                                  __builtin_bit_cast(F4, ds_read_tr16(qimg + o + 8 * pp + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+            for (int s16 = 0; s16 < FQ / 16; ++s16) {          // 16-feature k-steps of the chunk
+                F8 kf[2], qf[2];
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    const int o = (16 * s16 + 8 * h + qq) * KROW + (((blk * 2 + kh) ^ kswz(qq)) * 32);
+                    kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(kimg + o + 8 * sig)),
+                                                      __builtin_bit_cast(F4, ds_read_tr16(kimg + o + 8 * sig + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+                    qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(qimg + o + 8 * pp)),
+                                                      __builtin_bit_cast(F4, ds_read_tr16(qimg + o + 8 * pp + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb) sa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], sa[kb][qb]);
             }
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int qb = 0; qb < 2; ++qb) sa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], sa[kb][qb]);
         }
         __syncthreads();
     }
@@ -454,9 +459,9 @@ __global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, cons
     // ---- Oᵀ = Vᵀ·Pᵀ over feature chunks of 32, stored straight to the pixels ----
     const int wx = wx0 + wave;
     const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+    zero_region();                                             // v layout (last barrier of the q/k loop passed)
+    __syncthreads();
     for (int c0 = 0; c0 < DV; c0 += FV) {
-        zero_region();
-        __syncthreads();
         stage(v, dv, c0, FV, 0, VIMG, true);
         __syncthreads();
         if (wave < nwin) {
