@@ -225,13 +225,8 @@ __global__ __launch_bounds__(256, 2) void circ_fwd_tiled(CircParams P) {
                     if ((unsigned)(t * BN + kt - rq) >= (unsigned)W) sacc[kb][x] = kNegInf;
                 }
         }
-        float pm[4] = {sacc[0][0], sacc[0][1], sacc[0][2], sacc[0][3]};
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sacc[kb][x]);
-        const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
-        m_true = fmaxf(m_true, mt);
+        const float mt = swap_halves_max(lane_max<NKB>(sacc));
+        m_true = vmax(m_true, mt);
         if (__builtin_amdgcn_ballot_w64(mt > m_used + thr_raw) != 0) {
             // a band edge can leave a query without any key in this tile (mt = −inf)
             const float m_new = fmaxf(m_used, mt);

@@ -602,13 +602,8 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         F8 pf[NQB][NKB][2];
 #pragma unroll
         for (int u = 0; u < NQB; ++u) {
-            float pm[4] = {sacc[u][0][0], sacc[u][0][1], sacc[u][0][2], sacc[u][0][3]};
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sacc[u][kb][x]);
-            const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
-            m_true[u] = fmaxf(m_true[u], mt);
+            const float mt = swap_halves_max(lane_max<NKB>(sacc[u]));
+            m_true[u] = vmax(m_true[u], mt);
             if (__builtin_amdgcn_ballot_w64(mt > m_used[u] + thr_raw) != 0) {
                 const float m_new = fmaxf(m_used[u], mt);
                 const float alpha = exp2_fast((m_used[u] - m_new) * c);
