@@ -45,34 +45,23 @@ __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
 // Raw v_exp_f32 (2^x); exp2(-inf) = 0.
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// v_max_f32 / v_max3_f32 as single instructions.  fmaxf on an MFMA result gets
-// a NaN-canonicalising `v_max_f32 x, x, x` per operand under IEEE mode; MFMA
-// outputs are never signalling NaNs, and the NaN behaviour (maxNum: a quiet NaN
-// operand yields the other) is the same as fmaxf's.
-__device__ __forceinline__ float vmax(float a, float b) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// Max over the NB x 16 scores a lane holds: two interleaved v_max3 chains.
+// IEEE-2019 maximum (v_maximum3_f32 on gfx950): NaN-propagating like Julia's
+// `maximum`, and unlike fmaxf it needs no NaN-canonicalising `v_max_f32 x, x, x`
+// per MFMA-result operand.
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return vmax(vmax(a, b), c); }
+
+// Max over the NB x 16 scores a lane holds: four interleaved v_maximum3 chains.
 template <int NB>
 __device__ __forceinline__ float lane_max(const f32x16 (&s)[NB]) {
-    static_assert(NB * 16 >= 6, "lane_max");
-    float a = vmax3(s[0][0], s[0][1], s[0][2]);
-    float b = vmax3(s[0][3], s[0][4], s[0][5]);
-    int k = 6;
+    static_assert(NB * 16 >= 12 && (NB * 16 - 12) % 2 == 0, "lane_max");
+    float a[4];
 #pragma unroll
-    for (; k + 1 < NB * 16; k += 2) {
-        if ((k >> 1) & 1) a = vmax3(a, s[k >> 4][k & 15], s[(k + 1) >> 4][(k + 1) & 15]);
-        else              b = vmax3(b, s[k >> 4][k & 15], s[(k + 1) >> 4][(k + 1) & 15]);
-    }
-    if (k < NB * 16) a = vmax(a, s[k >> 4][k & 15]);
-    return vmax(a, b);
+    for (int c = 0; c < 4; ++c) a[c] = vmax3(s[0][3 * c], s[0][3 * c + 1], s[0][3 * c + 2]);
+#pragma unroll
+    for (int k = 12, c = 0; k < NB * 16; k += 2, c = (c + 1) & 3)
+        a[c] = vmax3(a[c], s[k >> 4][k & 15], s[(k + 1) >> 4][(k + 1) & 15]);
+    return vmax(vmax3(a[0], a[1], a[2]), a[3]);
 }
 
 // Value of x held by lane (l ^ 32): v_permlane32_swap on a copy.

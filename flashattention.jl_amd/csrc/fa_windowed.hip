@@ -226,8 +226,8 @@ __global__ __launch_bounds__(256, 2) void win_fused(const T* __restrict__ q, con
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-            for (int x = 0; x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sa[kb][x]);
-        const float mt = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+            for (int x = 0; x < 16; ++x) pm[x & 3] = vmax(pm[x & 3], sa[kb][x]);
+        const float mt = swap_halves_max(vmax(vmax(pm[0], pm[1]), vmax(pm[2], pm[3])));
         const float mc = mt * scale_log2;
         float ps[4] = {0.f, 0.f, 0.f, 0.f};
         F8 pf[NKB][2];
@@ -441,8 +441,8 @@ __global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, cons
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = fmaxf(pm[x & 3], sa[kb][qb][x]);
-        mt[qb] = swap_halves_max(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+            for (int x = (kb == 0 ? 4 : 0); x < 16; ++x) pm[x & 3] = vmax(pm[x & 3], sa[kb][qb][x]);
+        mt[qb] = swap_halves_max(vmax(vmax(pm[0], pm[1]), vmax(pm[2], pm[3])));
         const float mc = mt[qb] * scale_log2;
         float ps[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
