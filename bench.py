@@ -85,6 +85,28 @@ def time_launches(fn, steps, warmup, dist=None):
     return wall, ev_s
 
 
+def time_graph(fn, steps, dist=None):
+    """Device time per call of a launch-bound fn: `steps` calls captured in one
+    HIP graph (torch.cuda.graph) and replayed, so host issue overhead (Python +
+    ctypes, ~20-30 us per call) is not what gets measured for kernels of a few
+    microseconds.  Barrier + sync on both sides, max over ranks."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(steps):
+            fn()
+    graph.replay()
+    torch.cuda.synchronize()
+    _, e = time_launches(graph.replay, 3, 1, dist)
+    return e / 3 / steps
+
+
 def cpu_baseline(target_s: float = 12.0):
     """oracle/fa_cpu.c (C OpenMP port of dense_fa!, src/dense.jl:21-102, same
     Br=64/Bc=500 tiles) on a bounded sample of the same workload: whole
@@ -219,9 +241,7 @@ def extra_benches(fa_hip, args, dist):
     for Bimg in (1, 32):
         try:
             q, k, v = (_randn_jl(fa_hip, (128, 128, 64, Bimg), torch.bfloat16, gen) for _ in range(3))
-            steps = args.steps
-            w, e = time_launches(lambda: fa_hip.windowed_fa(q, k, v, 7), steps, 2, dist)
-            t = e / steps
+            t = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), args.steps, dist)
             T, L = 49, 19 * 19
             bytes_alg = Bimg * (3 * 128 * 128 * 64 * 2 + 128 * 128 * 64 * 2 + 2 * T * L * 4)
             res[f"cfg3_windowed_B{Bimg}_GBs"] = bytes_alg / t / 1e9
@@ -235,9 +255,7 @@ def extra_benches(fa_hip, args, dist):
         Qc, Kc, Vc = (_randn_jl(fa_hip, (Nc, dc, Bc), torch.bfloat16, gen) for _ in range(3))
         Oc = fa_hip.jl_empty((Nc, dc, Bc), torch.bfloat16)
         lc = fa_hip.jl_empty((Nc, 1, Bc)); mc = fa_hip.jl_empty((Nc, 1, Bc))
-        steps = args.steps
-        w, e = time_launches(lambda: fa_hip.circulant_fa_(Oc, lc, mc, Qc, Kc, Vc, Wc), steps, 2, dist)
-        t = e / steps
+        t = time_graph(lambda: fa_hip.circulant_fa_(Oc, lc, mc, Qc, Kc, Vc, Wc), args.steps, dist)
         tag = f"circ_N{Nc}_d{dc}_B{Bc}_W{Wc}"
         res[f"{tag}_us"] = t * 1e6
         res[f"{tag}_GBs"] = Bc * Nc * (4 * dc * 2 + 8) / t / 1e9       # Q, K, V, O + l, m

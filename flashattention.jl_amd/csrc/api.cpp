@@ -89,10 +89,11 @@ int fa_debug_set_bwd_generic(int v) {
     return old;
 }
 
-// Not part of the public header: 1 forces the composed windowed forward.
+// Not part of the public header: windowed forward path override (1 composed,
+// 2 register-gather fused, 3 / 4 one- / four-window row-staged where eligible; 0 auto).
 int fa_debug_set_win_composed(int v) {
     const int old = fa::g_win_force_composed;
-    fa::g_win_force_composed = (v == 1 || v == 2) ? v : 0;
+    fa::g_win_force_composed = (v >= 1 && v <= 4) ? v : 0;
     return old;
 }
 

@@ -504,7 +504,166 @@ __global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, cons
     }
 }
 
-int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused
+// --------------------------------------------------------------------------
+// Row-staged kernel, one window per workgroup (small launches: B = 1 of
+// configs[2] has 324 windows, so four windows per workgroup would leave most
+// CUs idle).  q, k and v are staged in ONE phase: every thread issues all its
+// image-aligned 16-B row loads before it scatters any of them (items decoded
+// with fixed strides — 2 chunks per row, 8 rows per feature — so out-of-window
+// items read an out-of-range offset, i.e. 0, and are skipped at the scatter),
+// so the workgroup pays one HBM round trip instead of one per item.  The 4
+// waves split the window: wave w computes query block (w & 1) and the 32-wide
+// v feature chunk (w >> 1).
+// --------------------------------------------------------------------------
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const T* __restrict__ k,
+                                                 const T* __restrict__ v, T* __restrict__ out,
+                                                 float* __restrict__ lo, float* __restrict__ mo,
+                                                 WinDev g, int d, int dv, float scale, float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int NTH = 256, KROW = 128, VROW = 144;
+    constexpr int QIMG = D * KROW, VIMG = DV * VROW, REGION = 2 * QIMG + VIMG;
+    constexpr int NBQ = D * 16 / NTH, NBV = DV * 16 / NTH;    // items per thread: feature x 8 rows x 2 chunks
+    static_assert(D * 16 % NTH == 0 && DV * 16 % NTH == 0, "item split");
+    __shared__ __attribute__((aligned(16))) char smem[REGION];
+    auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
+
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
+    const int bid = blockIdx.x;
+    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
+    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
+    const int c_lo = max(xs, 0) >> 3;
+    const int ncx = max(((min(xs + ws, W_) + 7) >> 3) - c_lo, 0);
+    const int ylo = max(y0, 0), nrow = max(min(y0 + ws, H_) - ylo, 0);
+
+    // item it -> (feature fl = it >> 4, row yy = (it >> 1) & 7, chunk cx = it & 1)
+    auto item_off = [&](int it, int C) {
+        const int cx = it & 1, yy = (it >> 1) & 7, fl = it >> 4;
+        const bool ok = cx < ncx && yy < nrow && fl < C;
+        return ok ? (fl * P_ + (ylo + yy) * W_ + (c_lo + cx) * 8) * 2 : 0x7FFFFFF0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    u32x4 rq[NBQ], rk[NBQ], rv[NBV];
+#pragma unroll
+    for (int j = 0; j < NBQ; ++j) {
+        const int o = item_off(tid + NTH * j, d);
+        rq[j] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o, 0, 0);
+        rk[j] = __builtin_amdgcn_raw_buffer_load_b128(krs, o, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NBV; ++j) rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, item_off(tid + NTH * j, dv), 0, 0);
+
+    for (int o = tid * 16; o < REGION; o += NTH * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    auto scatter = [&](const u32x4& val, int it, int C, char* base, bool vlayout) {
+        const int cx = it & 1, yy = (it >> 1) & 7, fl = it >> 4;
+        if (!(cx < ncx && yy < nrow && fl < C)) return;
+        const int ty = ylo + yy - y0;
+        int tx = (c_lo + cx) * 8 - xs;
+#pragma unroll
+        for (int e = 0; e < 8; ++e, ++tx) {
+            if (tx >= 0 && tx < ws) {
+                const unsigned wd = val[e >> 1];
+                const unsigned short px = (unsigned short)((e & 1) ? (wd >> 16) : (wd & 0xFFFFu));
+                const int slot = ty * 8 + tx;
+                const int o = vlayout ? fl * VROW + slot * 2 : fl * KROW + (((slot >> 4) ^ kswz(fl)) * 32) + (slot & 15) * 2;
+                *(unsigned short*)(base + o) = px;
+            }
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < NBQ; ++j) {
+        scatter(rq[j], tid + NTH * j, d, smem, false);
+        scatter(rk[j], tid + NTH * j, d, smem + QIMG, false);
+    }
+#pragma unroll
+    for (int j = 0; j < NBV; ++j) scatter(rv[j], tid + NTH * j, dv, smem + 2 * QIMG, true);
+    __syncthreads();
+
+    // ---- Sᵀ = K·Qᵀ for this wave's query block ----
+    const int qb = wave & 1, vc = wave >> 1;
+    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    f32x16 sa[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) sa[kb][x] = 0.0f;
+#pragma unroll
+    for (int s16 = 0; s16 < D / 16; ++s16) {
+        const int orow = (16 * s16 + 8 * h + qq) * KROW;
+        F8 kf[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+            const char* a = smem + QIMG + orow + (((blk * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
+            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        const char* a = smem + orow + (((qb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
+        const F8 qf = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sa[kb] = mfma32x32x16(kf[kb], qf, sa[kb]);
+    }
+
+    // ---- exact softmax per query (keys: the window's ws x ws real slots) ----
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+            if ((kt & 7) >= ws || (kt >> 3) >= ws) sa[kb][x] = kNegInf;
+        }
+    const float mt = swap_halves_max(lane_max<2>(sa));
+    const float mc = mt * scale_log2;
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};
+    F8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const float pr = exp2_fast(fmaf(sa[kb][x], scale_log2, -mc));
+            ps[x & 3] += pr;
+            pf[kb][x >> 3][x & 7] = (T)pr;
+        }
+    const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+
+    // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
+    const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
+    if (vc < DV / 32) {
+        const char* vimg = smem + 2 * QIMG + (vc * 32 + r) * VROW + 16 * h;
+        f32x16 oa;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) oa = mfma32x32x16(*(const F8*)(vimg + (kb * 32 + 16 * s2) * 2), pf[kb][s2], oa);
+        const int px = xs + qtx, py = y0 + qty;
+        if (qtx < ws && qty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+            const float inv = 1.0f / lt;
+            T* yb = out + (int64_t)b * dv * P_ + (int64_t)py * W_ + px;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = vc * 32 + acc_row(x, h);
+                if (cc < dv) yb[(int64_t)cc * P_] = (T)(oa[x] * inv);
+            }
+        }
+    }
+    if (vc == 0 && h == 0 && qtx < ws && qty < ws) {
+        const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+        const int64_t li = qty * ws + qtx + (int64_t)g.T * wid;
+        mo[li] = mt * scale;
+        lo[li] = lt;
+    }
+}
+
+int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 / 4 one- / four-window row-staged
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
@@ -525,15 +684,27 @@ static hipError_t launch_fused_dd(const WindowedArgs& a, const WinDev& g, void* 
 #undef FA_FUSED
     return hipGetLastError();
 }
-// Row-staged kernel: 2-D, non-overlapping (direct store), ws <= 8, width % 8 == 0,
-// 16-B aligned tensors (image-aligned 16-B row chunks).  Below ~1024 windows its
-// six serial feature-chunk phases are exposed (B = 1 of configs[2]: 38 vs 31 µs)
-// and the register-gather kernel is faster.
-static bool rows_ok(const WindowedArgs& a) {
-    return g_win_force_composed != 2 && a.g.L * a.batch >= 1024 && a.g.nsp == 2 &&
-           a.g.stride >= a.g.ws && a.g.ws <= 8 &&
-           a.g.S[0] % 8 == 0 && ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 &&
-           ((uintptr_t)a.v & 15u) == 0;
+// Row-staged kernels: 2-D, non-overlapping (direct store), ws <= 8, width % 8 == 0,
+// 16-B aligned tensors (image-aligned 16-B row chunks).  Four windows per
+// workgroup from kRows4Min windows up; one window per workgroup below (where four
+// per workgroup would leave CUs idle).  Returns 0 (not eligible), 1 or 4.
+constexpr int64_t kRows4Min = 1024;
+static int rows_kind(const WindowedArgs& a) {
+    if (g_win_force_composed == 1 || g_win_force_composed == 2) return 0;
+    const bool shape = a.g.nsp == 2 && a.g.stride >= a.g.ws && a.g.ws <= 8 && a.g.S[0] % 8 == 0 &&
+                       ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 && ((uintptr_t)a.v & 15u) == 0;
+    if (!shape) return 0;
+    if (g_win_force_composed == 3) return 1;
+    if (g_win_force_composed == 4) return 4;
+    return a.g.L * a.batch >= kRows4Min ? 4 : 1;
+}
+
+template <class T, int D, int DV>
+static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
+    hipLaunchKernelGGL((win_rows1<T, D, DV>), dim3((unsigned)(a.g.L * a.batch)), dim3(256), 0, s, (const T*)a.q,
+                       (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, a.scale,
+                       a.scale * kLog2e);
+    return hipGetLastError();
 }
 
 template <class T, int D, int DV>
@@ -549,11 +720,18 @@ static hipError_t launch_rows_dd(const WindowedArgs& a, const WinDev& g, hipStre
 template <class T>
 static hipError_t launch_fused(const WindowedArgs& a, const WinDev& g, void* out, bool direct, hipStream_t s) {
     const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
-    if (direct && out == a.y && rows_ok(a)) {
+    const int rk = direct && out == a.y ? rows_kind(a) : 0;
+    if (rk == 4) {
         if (Dc == 32 && DVc == 32) return launch_rows_dd<T, 32, 32>(a, g, s);
         if (Dc == 32) return launch_rows_dd<T, 32, 64>(a, g, s);
         if (DVc == 32) return launch_rows_dd<T, 64, 32>(a, g, s);
         return launch_rows_dd<T, 64, 64>(a, g, s);
+    }
+    if (rk == 1) {
+        if (Dc == 32 && DVc == 32) return launch_rows1_dd<T, 32, 32>(a, g, s);
+        if (Dc == 32) return launch_rows1_dd<T, 32, 64>(a, g, s);
+        if (DVc == 32) return launch_rows1_dd<T, 64, 32>(a, g, s);
+        return launch_rows1_dd<T, 64, 64>(a, g, s);
     }
     if (Dc == 32 && DVc == 32) return launch_fused_dd<T, 32, 32>(a, g, out, direct, s);
     if (Dc == 32) return launch_fused_dd<T, 32, 64>(a, g, out, direct, s);
