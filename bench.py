@@ -155,8 +155,10 @@ def _traffic_from_profiles():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
+    # ~0.1 s of untimed launches: from idle the GPU needs ~200 launches (~60 ms)
+    # to reach its sustained clock (tools/exp/ramp.py)
+    ap.add_argument("--warmup", type=int, default=400)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--extra", action="store_true", help="also time configs[2..3] (reported under 'extra')")
     args = ap.parse_args()

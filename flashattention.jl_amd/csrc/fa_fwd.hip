@@ -615,13 +615,15 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
                 m_used[u] = m_new;
             }
             const float mc = m_used[u] * c;
-            float ps[4] = {0.f, 0.f, 0.f, 0.f};
+            float ps[4];
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
                 for (int x = 0; x < 16; ++x) {
                     const float pv = exp2_fast(fmaf(sacc[u][kb][x], c, -mc));
-                    ps[x & 3] += pv;
+                    // first four seed the partial sums (no `0 + p` adds: without
+                    // fast-math the compiler must keep them, -0 + 0 != -0)
+                    if (kb == 0 && x < 4) ps[x] = pv; else ps[x & 3] += pv;
                     pf[u][kb][x >> 3][x & 7] = (T)pv;
                 }
             l_run[u] += (ps[0] + ps[1]) + (ps[2] + ps[3]);

@@ -37,7 +37,10 @@ def bench(name, fn, flops):
         diff = max((a.float() - b.float()).abs().max().item() for a, b in zip(outs[0], outs[i]))
         print(f"{name}: lib{i} vs lib0 bitwise equal={same} max|diff|={diff:.3e}", flush=True)
     times = [[] for _ in libs]
-    for rnd in range(6):
+    fa_hip._LIB = libs[0]
+    for _ in range(400):   # past the clock ramp (tools/exp/ramp.py: ~200 launches)
+        fn()
+    for rnd in range(int(os.environ.get("AB_ROUNDS", 8))):
         for i, L in enumerate(libs):
             fa_hip._LIB = L
             for _ in range(2):
@@ -65,6 +68,8 @@ for (N, d, BH) in [(4096, 64, 64), (8192, 128, 64)]:
     bench(f"dense N={N} d={d}", fwd, 4.0 * BH * N * N * d)
     del Q, K, V, O_
 
+if os.environ.get("AB_DENSE_ONLY"):
+    sys.exit(0)
 N, d, BH, W = 16384, 64, 64, 129
 Q, K, V = mk((N, d, BH), 2)
 O_ = fa_hip.jl_empty((N, d, BH), torch.bfloat16)
