@@ -93,7 +93,7 @@ int fa_debug_set_bwd_generic(int v) {
 // 2 register-gather fused, 3 / 4 one- / four-window row-staged where eligible; 0 auto).
 int fa_debug_set_win_composed(int v) {
     const int old = fa::g_win_force_composed;
-    fa::g_win_force_composed = (v >= 1 && v <= 4) ? v : 0;
+    fa::g_win_force_composed = (v >= 1 && v <= 5) ? v : 0;
     return old;
 }
 

@@ -24,6 +24,12 @@
 #include "fa_internal.h"
 #include "../../include/fa_hip.h"
 
+// Phase-timestamp hook for latency studies (tools/exp/win_stamp.hip defines it);
+// compiled out of the product library.
+#ifndef FA_STAMP
+#define FA_STAMP(k)
+#endif
+
 namespace fa {
 
 struct WinDev {
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void win_rows(const T* __restrict__ q, cons
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
-    int bid = blockIdx.x;
+    int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int gx = bid % ngx; bid /= ngx;
     const int wy = bid % g.O[1];
     const int b = bid / g.O[1];
@@ -529,6 +535,7 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
     __shared__ __attribute__((aligned(16))) char smem[REGION];
     auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
 
+    FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
@@ -560,6 +567,7 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
 
     for (int o = tid * 16; o < REGION; o += NTH * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
+    FA_STAMP(1);
     auto scatter = [&](const u32x4& val, int it, int C, char* base, bool vlayout) {
         const int cx = it & 1, yy = (it >> 1) & 7, fl = it >> 4;
         if (!(cx < ncx && yy < nrow && fl < C)) return;
@@ -584,6 +592,7 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
 #pragma unroll
     for (int j = 0; j < NBV; ++j) scatter(rv[j], tid + NTH * j, dv, smem + 2 * QIMG, true);
     __syncthreads();
+    FA_STAMP(2);
 
     // ---- Sᵀ = K·Qᵀ for this wave's query block ----
     const int qb = wave & 1, vc = wave >> 1;
@@ -611,6 +620,7 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
         for (int kb = 0; kb < 2; ++kb) sa[kb] = mfma32x32x16(kf[kb], qf, sa[kb]);
     }
 
+    FA_STAMP(3);
     // ---- exact softmax per query (keys: the window's ws x ws real slots) ----
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -632,6 +642,194 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
             pf[kb][x >> 3][x & 7] = (T)pr;
         }
     const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+
+    FA_STAMP(4);
+    // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
+    const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
+    if (vc < DV / 32) {
+        const char* vimg = smem + 2 * QIMG + (vc * 32 + r) * VROW + 16 * h;
+        f32x16 oa;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) oa = mfma32x32x16(*(const F8*)(vimg + (kb * 32 + 16 * s2) * 2), pf[kb][s2], oa);
+        const int px = xs + qtx, py = y0 + qty;
+        if (qtx < ws && qty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+            const float inv = 1.0f / lt;
+            T* yb = out + (int64_t)b * dv * P_ + (int64_t)py * W_ + px;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = vc * 32 + acc_row(x, h);
+                if (cc < dv) yb[(int64_t)cc * P_] = (T)(oa[x] * inv);
+            }
+        }
+    }
+    if (vc == 0 && h == 0 && qtx < ws && qty < ws) {
+        const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+        const int64_t li = qty * ws + qtx + (int64_t)g.T * wid;
+        mo[li] = mt * scale;
+        lo[li] = lt;
+    }
+    FA_STAMP(5);
+}
+
+// --------------------------------------------------------------------------
+// One window per workgroup, ws <= 7, row-SHIFT staging (the default row-staged
+// kernel for ws <= 7 at every launch size).  A window row of <= 7 pixels always
+// fits in the 8 pixels that start at the dword-aligned pixel
+//   a = clamp(xs & ~1, 0, W - 8),
+// so every (feature, window row) item is ONE 16-B buffer load, a wave-uniform
+// shift by sh = xs - a pixels (dword selects + v_alignbyte), a uniform mask
+// (slot < ws, pixel inside the image) and ONE ds_write_b128 into the dense
+// kernel's LDS layouts: 6 loads and 6 LDS writes per thread, no zero-fill and
+// no 2-byte scatter (the scatter kernel above spent ~30 % of its time there,
+// tools/exp/win_stamp.py).  Items cover all 8 slot rows and all D features,
+// so padding slots are written as zeros.  Workgroups are dealt to XCDs in
+// contiguous window runs (xcd_remap), so horizontally adjacent windows, which
+// share cache lines, hit one XCD's L2: configs[2] B=1 12.2 -> 6.8 us.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ unsigned pick_dword(const u32x4& in, int idx) {
+    unsigned r = 0u;
+    r = idx == 0 ? in[0] : r;
+    r = idx == 1 ? in[1] : r;
+    r = idx == 2 ? in[2] : r;
+    r = idx == 3 ? in[3] : r;
+    return r;
+}
+// out pixel t = in pixel (t + sh) (0 outside 0..7), sh in (-8, 8) wave-uniform,
+// then AND-ed with the per-slot mask.
+__device__ __forceinline__ u32x4 shift_row(const u32x4& in, int sh, const unsigned (&mask)[4]) {
+    const int s2 = sh >> 1;              // floor(sh / 2)
+    u32x4 o;
+    if (sh & 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            o[j] = __builtin_amdgcn_alignbyte(pick_dword(in, j + s2 + 1), pick_dword(in, j + s2), 2u) & mask[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pick_dword(in, j + s2) & mask[j];
+    }
+    return o;
+}
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const T* __restrict__ k,
+                                                  const T* __restrict__ v, T* __restrict__ out,
+                                                  float* __restrict__ lo, float* __restrict__ mo,
+                                                  WinDev g, int d, int dv, float scale, float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int NTH = 256, KROW = 128, VROW = 144;
+    constexpr int QIMG = D * KROW, VIMG = DV * VROW, REGION = 2 * QIMG + VIMG;
+    constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;    // items per thread: feature x 8 slot rows
+    static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
+    __shared__ __attribute__((aligned(16))) char smem[REGION];
+    auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
+
+    FA_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
+    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
+    const int ax = min(max(xs & ~1, 0), W_ - 8);
+    const int sh = xs - ax;
+
+    // item it -> (feature f = it >> 3, slot row yy = it & 7)
+    auto item_off = [&](int it, int C) {
+        const int yy = it & 7, f = it >> 3, y = y0 + yy;
+        const bool ok = yy < ws && y >= 0 && y < H_ && f < C;
+        return ok ? (f * P_ + y * W_ + ax) * 2 : 0x7FFFFFF0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    u32x4 rq[NIQ], rk[NIQ], rv[NIV];
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        const int o = item_off(tid + NTH * j, d);
+        rq[j] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o, 0, 0);
+        rk[j] = __builtin_amdgcn_raw_buffer_load_b128(krs, o, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, item_off(tid + NTH * j, dv), 0, 0);
+
+    // slot mask (uniform): slot t holds a pixel iff t < ws and 0 <= xs + t < W
+    unsigned mask[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int t0 = 2 * j, t1 = 2 * j + 1;
+        const bool v0 = t0 < ws && xs + t0 >= 0 && xs + t0 < W_;
+        const bool v1 = t1 < ws && xs + t1 >= 0 && xs + t1 < W_;
+        mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
+        const int ko = f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
+        *(u32x4*)(smem + ko) = shift_row(rq[j], sh, mask);
+        *(u32x4*)(smem + QIMG + ko) = shift_row(rk[j], sh, mask);
+    }
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
+        *(u32x4*)(smem + 2 * QIMG + f * VROW + yy * 16) = shift_row(rv[j], sh, mask);
+    }
+    __syncthreads();
+    FA_STAMP(2);
+
+    // ---- Sᵀ = K·Qᵀ for this wave's query block ----
+    const int qb = wave & 1, vc = wave >> 1;
+    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    f32x16 sa[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) sa[kb][x] = 0.0f;
+#pragma unroll
+    for (int s16 = 0; s16 < D / 16; ++s16) {
+        const int orow = (16 * s16 + 8 * h + qq) * KROW;
+        F8 kf[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+            const char* a = smem + QIMG + orow + (((blk * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
+            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        const char* a = smem + orow + (((qb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
+        const F8 qf = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sa[kb] = mfma32x32x16(kf[kb], qf, sa[kb]);
+    }
+    FA_STAMP(3);
+
+    // ---- exact softmax per query (keys: the window's ws x ws real slots) ----
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+            if ((kt & 7) >= ws || (kt >> 3) >= ws) sa[kb][x] = kNegInf;
+        }
+    const float mt = swap_halves_max(lane_max<2>(sa));
+    const float mc = mt * scale_log2;
+    float ps[4];
+    F8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const float pr = exp2_fast(fmaf(sa[kb][x], scale_log2, -mc));
+            if (kb == 0 && x < 4) ps[x] = pr; else ps[x & 3] += pr;
+            pf[kb][x >> 3][x & 7] = (T)pr;
+        }
+    const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+    FA_STAMP(4);
 
     // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
     const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
@@ -661,9 +859,10 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
         mo[li] = mt * scale;
         lo[li] = lt;
     }
+    FA_STAMP(5);
 }
 
-int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 / 4 one- / four-window row-staged
+int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 / 4 one- / four-window row-staged, 5 one-window scatter
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
@@ -685,22 +884,32 @@ static hipError_t launch_fused_dd(const WindowedArgs& a, const WinDev& g, void* 
     return hipGetLastError();
 }
 // Row-staged kernels: 2-D, non-overlapping (direct store), ws <= 8, width % 8 == 0,
-// 16-B aligned tensors (image-aligned 16-B row chunks).  Four windows per
-// workgroup from kRows4Min windows up; one window per workgroup below (where four
-// per workgroup would leave CUs idle).  Returns 0 (not eligible), 1 or 4.
+// 16-B aligned tensors.  ws <= 7: the one-window row-shift kernel at every size.
+// ws = 8 (row scatter): four windows per workgroup from kRows4Min windows up, one
+// window per workgroup below (where four per workgroup would leave CUs idle).
+// Returns 0 (not eligible), 1 or 4.
 constexpr int64_t kRows4Min = 1024;
 static int rows_kind(const WindowedArgs& a) {
     if (g_win_force_composed == 1 || g_win_force_composed == 2) return 0;
     const bool shape = a.g.nsp == 2 && a.g.stride >= a.g.ws && a.g.ws <= 8 && a.g.S[0] % 8 == 0 &&
                        ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 && ((uintptr_t)a.v & 15u) == 0;
     if (!shape) return 0;
-    if (g_win_force_composed == 3) return 1;
+    if (g_win_force_composed == 3 || g_win_force_composed == 5) return 1;
     if (g_win_force_composed == 4) return 4;
+    // ws <= 7: the one-window row-shift kernel beats the four-window one at
+    // every batch size (128x128x64, ws 7: B=1 7.2 vs 26.6 us, B=32 96 vs 120 us)
+    if (a.g.ws <= 7) return 1;
     return a.g.L * a.batch >= kRows4Min ? 4 : 1;
 }
 
 template <class T, int D, int DV>
 static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
+    if (a.g.ws <= 7 && g_win_force_composed != 5) {
+        hipLaunchKernelGGL((win_rows1s<T, D, DV>), dim3((unsigned)(a.g.L * a.batch)), dim3(256), 0, s,
+                           (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
+                           (int)a.dv, a.scale, a.scale * kLog2e);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((win_rows1<T, D, DV>), dim3((unsigned)(a.g.L * a.batch)), dim3(256), 0, s, (const T*)a.q,
                        (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, a.scale,
                        a.scale * kLog2e);

@@ -1,0 +1,69 @@
+"""GPU parity of every fused windowed-forward kernel, each forced in turn
+(fa_debug_set_win_composed: 1 composed gather→dense→fold, 2 register-gather,
+3 one-window row-shift (ws <= 7) / row-scatter (ws = 8), 4 four-window
+row-staged, 5 one-window row-scatter), against the oracle restatement of
+windowed_fa (src/windowed.jl:3-23, NNlib unfold/fold geometry) on geometries
+chosen for the row-staged kernels' edge handling: windows hanging over the
+left / right / bottom image edge, odd and even window x-starts (the row-shift
+kernel's dword-aligned 16-B loads), pad >= ws, stride > ws (uncovered pixels
+are NaN), ws = 8, and head dims below / between the compiled classes."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_close, assert_lm_close
+from oracle import fa_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [  # (W, H, ws, stride, pad)
+    (16, 16, 3, 3, 1),
+    (24, 13, 5, 5, 2),
+    (32, 20, 7, 7, 3),
+    (16, 9, 7, 9, 0),
+    (8, 8, 7, 7, 6),
+    (40, 24, 6, 6, 2),
+    (24, 16, 8, 8, 3),
+    (48, 17, 7, 8, 1),
+]
+DIMS = [(64, 64), (32, 64), (64, 32), (20, 48)]
+
+
+@pytest.fixture(scope="module")
+def fa():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    import fa_hip
+    fa_hip.lib()
+    return fa_hip
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_forced_path(fa, geom, path):
+    W, H, ws, st, pad = geom
+    rng = np.random.default_rng(W * 1000 + H * 10 + ws)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        for (d, dv) in DIMS:
+            B = 2
+            q, k = (bf(rng.standard_normal((W, H, d, B))) for _ in range(2))
+            v = bf(rng.standard_normal((W, H, dv, B)))
+            y, l, m = fa.windowed_fa(*(fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v)), ws,
+                                     stride=st, pad=pad)
+            torch.cuda.synchronize()
+            yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
+            tag = f"path {path} d {d} dv {dv}"
+            assert_close(_np(y), yr, "bfloat16", f"y ({tag})", nan_ok=True)
+            assert_lm_close(_np(l), lr, "bfloat16", f"l ({tag})")
+            assert_lm_close(_np(m), mr, "bfloat16", f"m ({tag})")
+    finally:
+        L.fa_debug_set_win_composed(old)
