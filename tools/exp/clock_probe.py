@@ -1,7 +1,7 @@
-"""Run the configs[1] forward back-to-back for a few seconds while sampling the
-GPU's clock and power with rocm-smi in a child process: tells whether the
-forward is power/clock-capped (DVFS) or issue-bound at full clock.
-Usage: python tools/exp/clock_probe.py [seconds]"""
+"""Run a workload back-to-back for a few seconds while sampling the GPU's clock
+and power with rocm-smi in child processes: tells whether a kernel is
+power/clock-capped (DVFS) or issue-bound at full clock.
+Usage: python tools/exp/clock_probe.py [seconds] [fwd|fwd128|gemm|bwd]..."""
 import os, subprocess, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
@@ -9,39 +9,65 @@ import torch
 import fa_hip
 
 secs = float(sys.argv[1]) if len(sys.argv) > 1 else 6.0
-N, d, BH = int(os.environ.get("FA_N", 4096)), int(os.environ.get("FA_D", 64)), int(os.environ.get("FA_BH", 64))
+modes = sys.argv[2:] or ["fwd"]
 g = torch.Generator(device="cuda").manual_seed(0)
-Q, K, V = [fa_hip.jl_empty((N, d, BH), torch.bfloat16) for _ in range(3)]
-for t in (Q, K, V):
-    t.copy_(torch.randn((N, d, BH), generator=g, device="cuda"))
-O = fa_hip.jl_empty((N, d, BH), torch.bfloat16)
-l = fa_hip.jl_empty((N, 1, BH)); m = fa_hip.jl_empty((N, 1, BH))
+
+
+def jl(shape):
+    t = fa_hip.jl_empty(shape, torch.bfloat16)
+    t.copy_(torch.randn(shape, generator=g, device="cuda"))
+    return t
+
+
+def workload(mode):
+    if mode in ("fwd", "fwd128", "bwd"):
+        N, d, BH = (4096, 64, 64) if mode == "fwd" else (8192, 128, 64)
+        Q, K, V = jl((N, d, BH)), jl((N, d, BH)), jl((N, d, BH))
+        O = fa_hip.jl_empty((N, d, BH), torch.bfloat16)
+        l = fa_hip.jl_empty((N, 1, BH)); m = fa_hip.jl_empty((N, 1, BH))
+        fa_hip.dense_fa_(O, l, m, Q, K, V)
+        if mode == "bwd":
+            dO = jl((N, d, BH))
+            return (lambda: fa_hip.dense_fa_backward(Q, K, V, O, dO, l, m)), 10.0 * BH * N * N * d
+        return (lambda: fa_hip.dense_fa_(O, l, m, Q, K, V)), 4.0 * BH * N * N * d
+    n = 8192
+    a = torch.randn((n, n), device="cuda", dtype=torch.bfloat16)
+    b = torch.randn((n, n), device="cuda", dtype=torch.bfloat16)
+    c = torch.empty((n, n), device="cuda", dtype=torch.bfloat16)
+    return (lambda: torch.matmul(a, b, out=c)), 2.0 * n ** 3
 
 
 def smi():
-    try:
-        return subprocess.run(["rocm-smi", "--showpower", "--showclocks", "--showtemp"],
-                              capture_output=True, text=True, timeout=20).stdout
-    except Exception as e:  # noqa: BLE001
-        return f"rocm-smi failed: {e}"
+    return subprocess.Popen(["rocm-smi", "--showpower", "--showclocks"],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
 
 
-print("== idle\n" + smi(), flush=True)
-t_end = time.time() + secs
-n = 0
-e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-e0.record()
-probe_at = time.time() + secs / 2
-probed = False
-while time.time() < t_end:
-    for _ in range(50):
-        fa_hip.dense_fa_(O, l, m, Q, K, V)
-    n += 50
-    if not probed and time.time() > probe_at:
-        probed = True
-        proc = subprocess.Popen(["rocm-smi", "--showpower", "--showclocks", "--showtemp"],
-                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-e1.record(); torch.cuda.synchronize()
-print("== under load\n" + proc.communicate(timeout=60)[0], flush=True)
-t = e0.elapsed_time(e1) / 1e3 / n
-print(f"{n} launches, {t*1e6:.1f} us each, {4.0*BH*N*N*d/t/1e12:.1f} TFLOP/s", flush=True)
+def parse(txt):
+    pw = [l.split(":")[-1].strip() for l in txt.splitlines() if "Power (W)" in l]
+    sc = [l.split("(")[-1].rstrip(")") for l in txt.splitlines() if "sclk" in l]
+    return f"power {pw[0] if pw else '?'} W, sclk {sc[0] if sc else '?'}"
+
+
+for mode in modes:
+    fn, flops = workload(mode)
+    for _ in range(20):
+        fn()
+    torch.cuda.synchronize()
+    t_end = time.time() + secs
+    n, probes, next_probe = 0, [], time.time() + secs / 4
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    while time.time() < t_end:
+        for _ in range(10):
+            fn()
+        n += 10
+        if time.time() > next_probe and len(probes) < 3:
+            probes.append(smi())
+            next_probe += secs / 5
+    e1.record(); torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / n
+    readings = "; ".join(parse(p.communicate(timeout=60)[0]) for p in probes)
+    print(f"{mode}: {n} launches, {t*1e6:.1f} us each, {flops/t/1e12:.1f} TFLOP/s | {readings}", flush=True)
+    del fn
+    torch.cuda.empty_cache()
+    time.sleep(2)
