@@ -714,6 +714,13 @@ __device__ __forceinline__ u32x4 shift_row(const u32x4& in, int sh, const unsign
     return o;
 }
 
+// Workgroup barrier that orders LDS only (s_waitcnt lgkmcnt(0); s_barrier):
+// outstanding global loads are not waited for.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
+    __builtin_amdgcn_s_barrier();
+}
+
 template <class T, int D, int DV>
 __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const T* __restrict__ k,
                                                   const T* __restrict__ v, T* __restrict__ out,
@@ -773,12 +780,9 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
         *(u32x4*)(smem + ko) = shift_row(rq[j], sh, mask);
         *(u32x4*)(smem + QIMG + ko) = shift_row(rk[j], sh, mask);
     }
-#pragma unroll
-    for (int j = 0; j < NIV; ++j) {
-        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
-        *(u32x4*)(smem + 2 * QIMG + f * VROW + yy * 16) = shift_row(rv[j], sh, mask);
-    }
-    __syncthreads();
+    // LDS-only barrier: the v loads stay in flight across it (a __syncthreads
+    // fence would wait for them) and land under the QK / softmax phase
+    lds_barrier();
     FA_STAMP(2);
 
     // ---- Sᵀ = K·Qᵀ for this wave's query block ----
@@ -830,6 +834,13 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
         }
     const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
     FA_STAMP(4);
+
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
+        *(u32x4*)(smem + 2 * QIMG + f * VROW + yy * 16) = shift_row(rv[j], sh, mask);
+    }
+    lds_barrier();
 
     // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
     const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
