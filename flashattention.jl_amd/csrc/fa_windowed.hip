@@ -676,8 +676,8 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
 }
 
 // --------------------------------------------------------------------------
-// One window per workgroup, ws <= 7, row-SHIFT staging (the default row-staged
-// kernel for ws <= 7 at every launch size).  A window row of <= 7 pixels always
+// Row-SHIFT staging, ws <= 7 (the default row-staged kernel for ws <= 7 at
+// every launch size; two windows per workgroup, below).  A window row of <= 7 pixels always
 // fits in the 8 pixels that start at the dword-aligned pixel
 //   a = clamp(xs & ~1, 0, W - 8),
 // so every (feature, window row) item is ONE 16-B buffer load, a wave-uniform
@@ -688,7 +688,8 @@ __global__ __launch_bounds__(256) void win_rows1(const T* __restrict__ q, const 
 // tools/exp/win_stamp.py).  Items cover all 8 slot rows and all D features,
 // so padding slots are written as zeros.  Workgroups are dealt to XCDs in
 // contiguous window runs (xcd_remap), so horizontally adjacent windows, which
-// share cache lines, hit one XCD's L2: configs[2] B=1 12.2 -> 6.8 us.
+// share cache lines, hit one XCD's L2: configs[2] B=1 12.2 -> 6.8 us.  Two
+// windows per workgroup (their loads coalesce, below) took B=32 97 -> 83 us.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ unsigned pick_dword(const u32x4& in, int idx) {
     unsigned r = 0u;
@@ -721,39 +722,74 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-template <class T, int D, int DV>
-__global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const T* __restrict__ k,
-                                                  const T* __restrict__ v, T* __restrict__ out,
-                                                  float* __restrict__ lo, float* __restrict__ mo,
-                                                  WinDev g, int d, int dv, float scale, float scale_log2) {
+// Per-lane variant of shift_row (windows of one workgroup differ in shift).
+__device__ __forceinline__ u32x4 shift_row_lane(const u32x4& in, int sh, const unsigned (&mask)[4]) {
+    const int s2 = sh >> 1;
+    const bool odd = (sh & 1) != 0;
+    unsigned e[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) e[j] = pick_dword(in, j + s2);
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (odd ? __builtin_amdgcn_alignbyte(e[j + 1], e[j], 2u) : e[j]) & mask[j];
+    return o;
+}
+
+// NWIN horizontally adjacent windows per workgroup (4 waves each).  Staging items
+// interleave the windows on adjacent lanes, so the NWIN 16-B row loads of one
+// (feature, row) — 14 B apart at stride 7 — fall in the same cache line and
+// coalesce in the texture path (NWIN = 1: the wave-uniform shift above).
+template <class T, int D, int DV, int NWIN>
+__global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q, const T* __restrict__ k,
+                                                         const T* __restrict__ v, T* __restrict__ out,
+                                                         float* __restrict__ lo, float* __restrict__ mo,
+                                                         WinDev g, int d, int dv, int64_t nwin_total,
+                                                         float scale, float scale_log2) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
-    constexpr int NTH = 256, KROW = 128, VROW = 144;
+    constexpr int NTH = 256 * NWIN, KROW = 128, VROW = 144;
     constexpr int QIMG = D * KROW, VIMG = DV * VROW, REGION = 2 * QIMG + VIMG;
-    constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;    // items per thread: feature x 8 slot rows
-    static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
-    __shared__ __attribute__((aligned(16))) char smem[REGION];
+    constexpr int NIQ = D * 8 / 256, NIV = DV * 8 / 256;    // items per thread: window x feature x 8 slot rows
+    static_assert(D * 8 % 256 == 0 && DV * 8 % 256 == 0, "item split");
+    __shared__ __attribute__((aligned(16))) char smem[NWIN * REGION];
     auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
 
     FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
-    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
-    const int ax = min(max(xs & ~1, 0), W_ - 8);
-    const int sh = xs - ax;
-
-    // item it -> (feature f = it >> 3, slot row yy = it & 7)
-    auto item_off = [&](int it, int C) {
-        const int yy = it & 7, f = it >> 3, y = y0 + yy;
-        const bool ok = yy < ws && y >= 0 && y < H_ && f < C;
-        return ok ? (f * P_ + y * W_ + ax) * 2 : 0x7FFFFFF0;
+    const int64_t wid0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * NWIN;
+    const int nperimg = g.O[0] * g.O[1];
+    struct Win { int wx, wy, b, xs, y0, ax; bool ok; };
+    auto win_of = [&](int wl) {
+        Win w;
+        const int64_t id = wid0 + wl;
+        w.ok = id < nwin_total;
+        const int64_t idc = w.ok ? id : 0;
+        w.b = (int)(idc / nperimg);
+        const int rem = (int)(idc - (int64_t)w.b * nperimg);
+        w.wy = rem / g.O[0];
+        w.wx = rem - w.wy * g.O[0];
+        w.xs = w.wx * st - g.pad;
+        w.y0 = w.wy * st - g.pad;
+        w.ax = min(max(w.xs & ~1, 0), W_ - 8);
+        return w;
     };
-    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+
+    // item it -> (window it % NWIN, feature f = (it / NWIN) >> 3, slot row yy = (it / NWIN) & 7)
+    // descriptors over the workgroup's first image and the next one (a window
+    // pair may straddle images); item offsets are relative to image b0
+    const int b0 = win_of(0).b;
+    const int nimg = min(NWIN == 1 ? 1 : 2, (int)(nwin_total / nperimg) - b0);
+    auto item_off = [&](int it, int C) {
+        const Win w = win_of(NWIN == 1 ? 0 : it % NWIN);
+        const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3, y = w.y0 + yy;
+        const bool ok = w.ok && yy < ws && y >= 0 && y < H_ && f < C;
+        return ok ? (((w.b - b0) * C + f) * P_ + y * W_ + w.ax) * 2 : 0x7FFFFFF0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b0 * d * P_, (uint32_t)(nimg * d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b0 * d * P_, (uint32_t)(nimg * d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b0 * dv * P_, (uint32_t)(nimg * dv * P_ * 2));
     u32x4 rq[NIQ], rk[NIQ], rv[NIV];
 #pragma unroll
     for (int j = 0; j < NIQ; ++j) {
@@ -764,29 +800,39 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
 #pragma unroll
     for (int j = 0; j < NIV; ++j) rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, item_off(tid + NTH * j, dv), 0, 0);
 
-    // slot mask (uniform): slot t holds a pixel iff t < ws and 0 <= xs + t < W
-    unsigned mask[4];
+    // staging of one item: shift into slots, mask (slot < ws, pixel inside the image)
+    auto stage = [&](const u32x4& val, int it, char* img, bool vlayout) {
+        const int wl = NWIN == 1 ? 0 : it % NWIN;
+        const Win w = win_of(wl);
+        const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3;
+        unsigned mask[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int t0 = 2 * j, t1 = 2 * j + 1;
-        const bool v0 = t0 < ws && xs + t0 >= 0 && xs + t0 < W_;
-        const bool v1 = t1 < ws && xs + t1 >= 0 && xs + t1 < W_;
-        mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
-    }
+        for (int j = 0; j < 4; ++j) {
+            const int t0 = 2 * j, t1 = 2 * j + 1;
+            const bool v0 = t0 < ws && w.xs + t0 >= 0 && w.xs + t0 < W_;
+            const bool v1 = t1 < ws && w.xs + t1 >= 0 && w.xs + t1 < W_;
+            mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
+        }
+        const u32x4 o = NWIN == 1 ? shift_row(val, w.xs - w.ax, mask) : shift_row_lane(val, w.xs - w.ax, mask);
+        char* base = smem + wl * REGION + (img - smem);
+        const int off = vlayout ? f * VROW + yy * 16 : f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
+        *(u32x4*)(base + off) = o;
+    };
 #pragma unroll
     for (int j = 0; j < NIQ; ++j) {
-        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
-        const int ko = f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
-        *(u32x4*)(smem + ko) = shift_row(rq[j], sh, mask);
-        *(u32x4*)(smem + QIMG + ko) = shift_row(rk[j], sh, mask);
+        stage(rq[j], tid + NTH * j, smem, false);
+        stage(rk[j], tid + NTH * j, smem + QIMG, false);
     }
     // LDS-only barrier: the v loads stay in flight across it (a __syncthreads
     // fence would wait for them) and land under the QK / softmax phase
     lds_barrier();
     FA_STAMP(2);
 
-    // ---- Sᵀ = K·Qᵀ for this wave's query block ----
-    const int qb = wave & 1, vc = wave >> 1;
+    // ---- this wave's window, query block and v chunk ----
+    const int wl = wave >> 2;
+    const Win w = win_of(wl);
+    char* const wsm = smem + wl * REGION;
+    const int qb = wave & 1, vc = (wave >> 1) & 1;
     const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
     const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
     f32x16 sa[2];
@@ -800,11 +846,11 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
         F8 kf[2];
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
-            const char* a = smem + QIMG + orow + (((blk * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
+            const char* a = wsm + QIMG + orow + (((blk * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
             kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
                                               __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
         }
-        const char* a = smem + orow + (((qb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
+        const char* a = wsm + orow + (((qb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
         const F8 qf = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
                                               __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
@@ -836,16 +882,13 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
     FA_STAMP(4);
 
 #pragma unroll
-    for (int j = 0; j < NIV; ++j) {
-        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
-        *(u32x4*)(smem + 2 * QIMG + f * VROW + yy * 16) = shift_row(rv[j], sh, mask);
-    }
+    for (int j = 0; j < NIV; ++j) stage(rv[j], tid + NTH * j, smem + 2 * QIMG, true);
     lds_barrier();
 
     // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
     const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
-    if (vc < DV / 32) {
-        const char* vimg = smem + 2 * QIMG + (vc * 32 + r) * VROW + 16 * h;
+    if (vc < DV / 32 && w.ok) {
+        const char* vimg = wsm + 2 * QIMG + (vc * 32 + r) * VROW + 16 * h;
         f32x16 oa;
 #pragma unroll
         for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
@@ -853,10 +896,10 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) oa = mfma32x32x16(*(const F8*)(vimg + (kb * 32 + 16 * s2) * 2), pf[kb][s2], oa);
-        const int px = xs + qtx, py = y0 + qty;
+        const int px = w.xs + qtx, py = w.y0 + qty;
         if (qtx < ws && qty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
             const float inv = 1.0f / lt;
-            T* yb = out + (int64_t)b * dv * P_ + (int64_t)py * W_ + px;
+            T* yb = out + (int64_t)w.b * dv * P_ + (int64_t)py * W_ + px;
 #pragma unroll
             for (int x = 0; x < 16; ++x) {
                 const int cc = vc * 32 + acc_row(x, h);
@@ -864,8 +907,8 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
             }
         }
     }
-    if (vc == 0 && h == 0 && qtx < ws && qty < ws) {
-        const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+    if (vc == 0 && h == 0 && qtx < ws && qty < ws && w.ok) {
+        const int64_t wid = (int64_t)(w.wx + g.O[0] * w.wy) + (int64_t)g.L * w.b;
         const int64_t li = qty * ws + qtx + (int64_t)g.T * wid;
         mo[li] = mt * scale;
         lo[li] = lt;
@@ -873,7 +916,7 @@ __global__ __launch_bounds__(256) void win_rows1s(const T* __restrict__ q, const
     FA_STAMP(5);
 }
 
-int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 / 4 one- / four-window row-staged, 5 one-window scatter
+int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default)
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
@@ -905,10 +948,11 @@ static int rows_kind(const WindowedArgs& a) {
     const bool shape = a.g.nsp == 2 && a.g.stride >= a.g.ws && a.g.ws <= 8 && a.g.S[0] % 8 == 0 &&
                        ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 && ((uintptr_t)a.v & 15u) == 0;
     if (!shape) return 0;
-    if (g_win_force_composed == 3 || g_win_force_composed == 5) return 1;
+    if (g_win_force_composed == 3 || g_win_force_composed >= 5) return 1;
     if (g_win_force_composed == 4) return 4;
-    // ws <= 7: the one-window row-shift kernel beats the four-window one at
-    // every batch size (128x128x64, ws 7: B=1 7.2 vs 26.6 us, B=32 96 vs 120 us)
+    // ws <= 7: the row-shift kernel (two windows per workgroup) beats the
+    // four-window row-scatter one at every batch size (128x128x64, ws 7:
+    // B=1 6.8 vs 26.7 us, B=32 83-90 vs 123 us)
     if (a.g.ws <= 7) return 1;
     return a.g.L * a.batch >= kRows4Min ? 4 : 1;
 }
@@ -916,9 +960,17 @@ static int rows_kind(const WindowedArgs& a) {
 template <class T, int D, int DV>
 static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
     if (a.g.ws <= 7 && g_win_force_composed != 5) {
-        hipLaunchKernelGGL((win_rows1s<T, D, DV>), dim3((unsigned)(a.g.L * a.batch)), dim3(256), 0, s,
-                           (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
-                           (int)a.dv, a.scale, a.scale * kLog2e);
+        const int64_t nw = a.g.L * a.batch;
+        const bool two_img_ok = 2 * a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX;
+        if (g_win_force_composed != 3 && two_img_ok) {   // default: two windows per workgroup
+            hipLaunchKernelGGL((win_rows1s<T, D, DV, 2>), dim3((unsigned)((nw + 1) / 2)), dim3(512), 0, s,
+                               (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
+                               (int)a.dv, nw, a.scale, a.scale * kLog2e);
+        } else {
+            hipLaunchKernelGGL((win_rows1s<T, D, DV, 1>), dim3((unsigned)nw), dim3(256), 0, s,
+                               (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
+                               (int)a.dv, nw, a.scale, a.scale * kLog2e);
+        }
         return hipGetLastError();
     }
     hipLaunchKernelGGL((win_rows1<T, D, DV>), dim3((unsigned)(a.g.L * a.batch)), dim3(256), 0, s, (const T*)a.q,

@@ -1,7 +1,7 @@
-"""configs[2] windowed forward, B sweep: auto (0) vs one-window row-staged (3) vs
-four-window row-staged (4) vs register-gather (2) vs composed (1).  Device time per
-call from HIP-graph replay (bench.time_graph), GB/s of algorithmic traffic; outputs
-compared against the composed path."""
+"""configs[2] windowed forward, B sweep: auto (0) vs one-window row-shift (3) vs
+two-window row-shift (6) vs four-window row-scatter (4) vs register-gather (2).
+Device time per call from HIP-graph replay (bench.time_graph), GB/s of algorithmic
+traffic; outputs compared against the four-window path."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
@@ -10,7 +10,7 @@ import fa_hip
 from bench import time_graph
 L = fa_hip.lib()
 L.fa_debug_set_win_composed.argtypes = [ctypes.c_int]
-NAMES = {0: "auto    ", 3: "rows1   ", 4: "rows4   ", 2: "gather  ", 1: "composed"}
+NAMES = {0: "auto    ", 3: "rows1   ", 6: "rows1x2 ", 4: "rows4   ", 2: "gather  ", 1: "composed"}
 Bs = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8, 32, 128]
 for B in Bs:
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -18,14 +18,14 @@ for B in Bs:
     T, Lw = 49, 361
     alg = B * (4 * 128 * 128 * 64 * 2 + 2 * T * Lw * 4)
     res = {}
-    for comp in (0, 3, 4, 2, 1):
+    for comp in (0, 3, 6, 4, 2):
         L.fa_debug_set_win_composed(comp)
         y, l, m = fa_hip.windowed_fa(q, k, v, 7)
         torch.cuda.synchronize()
         res[comp] = (y.float(), l.clone())
         t = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), 20)
         print(f"B={B:4d} {NAMES[comp]}: {t*1e6:9.1f} us  {alg/t/1e9:8.1f} GB/s", flush=True)
-    for c in (0, 3, 4, 2):
-        dy = (res[c][0] - res[1][0]).abs().max()
-        print(f"   {c} vs composed: max|dy| {float(dy):.3e}  max|dl| {float((res[c][1]-res[1][1]).abs().max()):.3e}")
+    for c in (0, 3, 6, 2):
+        dy = (res[c][0] - res[4][0]).abs().max()
+        print(f"   {c} vs rows4: max|dy| {float(dy):.3e}  max|dl| {float((res[c][1]-res[4][1]).abs().max()):.3e}")
     L.fa_debug_set_win_composed(0)
