@@ -180,6 +180,32 @@ int fa_windowed_fwd(int dtype, const void* q, const void* k, const void* v, void
     return rc == FA_OK ? ok() : fail(rc, fn, why);
 }
 
+static int window_common(const char* fn, int dtype, const void* src, void* dst, int nspatial,
+                         const int64_t* spatial, int64_t C, int64_t batch, int64_t ws, int64_t stride,
+                         int64_t pad, bool unwindow, void* hip_stream) {
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (C < 1 || batch < 1) return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: C, batch must be >= 1");
+    if (!src || !dst) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    fa::WindowGeom g{};
+    const char* why = "";
+    int rc = make_geom(g, nspatial, spatial, ws, stride, pad, &why);
+    if (rc != FA_OK) return fail(rc, fn, why);
+    rc = fa::launch_window(dtype, src, dst, g, C, batch, unwindow, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
+int fa_window(int dtype, const void* x, void* xw, int nspatial, const int64_t* spatial, int64_t C,
+              int64_t batch, int64_t ws, int64_t stride, int64_t pad, void* hip_stream) {
+    return window_common("fa_window", dtype, x, xw, nspatial, spatial, C, batch, ws, stride, pad, false,
+                         hip_stream);
+}
+
+int fa_unwindow(int dtype, const void* xw, void* x, int nspatial, const int64_t* spatial, int64_t C,
+                int64_t batch, int64_t ws, int64_t stride, int64_t pad, void* hip_stream) {
+    return window_common("fa_unwindow", dtype, xw, x, nspatial, spatial, C, batch, ws, stride, pad, true,
+                         hip_stream);
+}
+
 int fa_windowed_bwd(int dtype, const void* q, const void* k, const void* v, const void* y, const void* dy,
                     const float* l, const float* m, void* dq, void* dk, void* dv_, int nspatial,
                     const int64_t* spatial, int64_t d, int64_t dv, int64_t batch, int64_t ws,

@@ -90,6 +90,9 @@ size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why);
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why);
 int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why);
+// window (unfold) / unwindow (fold, sum over overlaps) of one tensor (S..., C, B) <-> (T, C, L, B)
+int launch_window(int dtype, const void* src, void* dst, const WindowGeom& g, int64_t C, int64_t batch,
+                  bool unwindow, hipStream_t s, const char** why);
 size_t softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims);
 int launch_softmax(const SoftmaxArgs& a, hipStream_t s, const char** why);
 

@@ -1104,6 +1104,36 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
     return FA_OK;
 }
 
+int launch_window(int dtype, const void* src, void* dst, const WindowGeom& geom, int64_t C, int64_t batch,
+                  bool unwindow, hipStream_t s, const char** why) {
+    if (!geom_fits(geom, C, C, batch) || C > INT32_MAX) {
+        *why = "window geometry exceeds the 32-bit index range";
+        return FA_ERR_UNSUPPORTED;
+    }
+    const WinDev g = to_dev(geom);
+    const int64_t total = unwindow ? geom.P * C * batch : geom.T * C * geom.L * batch;
+    if (total == 0) return FA_OK;
+    if ((total + 255) / 256 > INT32_MAX) {
+        *why = "grid too large";
+        return FA_ERR_UNSUPPORTED;
+    }
+    hipError_t e;
+    switch (dtype) {
+        case FA_DTYPE_BF16: e = unwindow ? fold<bf16>(src, dst, (int)C, batch, g, false, s)
+                                         : gather<bf16>(src, dst, (int)C, batch, g, false, s); break;
+        case FA_DTYPE_F16: e = unwindow ? fold<f16>(src, dst, (int)C, batch, g, false, s)
+                                        : gather<f16>(src, dst, (int)C, batch, g, false, s); break;
+        case FA_DTYPE_F32: e = unwindow ? fold<float>(src, dst, (int)C, batch, g, false, s)
+                                        : gather<float>(src, dst, (int)C, batch, g, false, s); break;
+        default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
+    }
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return FA_ERR_HIP;
+    }
+    return FA_OK;
+}
+
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
         *why = "head dimension exceeds the compiled maximum (128)";

@@ -112,6 +112,10 @@ def lib() -> ctypes.CDLL:
     L.fa_windowed_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                   ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64,
                                   f32, vp, ctypes.c_size_t, vp]
+    for wfn in ("fa_window", "fa_unwindow"):
+        getattr(L, wfn).restype = ctypes.c_int
+        getattr(L, wfn).argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.POINTER(i64), i64, i64,
+                                    i64, i64, i64, vp]
     L.fa_circulant_fwd.restype = ctypes.c_int
     L.fa_circulant_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp]
     L.fa_softmax_workspace.restype = ctypes.c_size_t
@@ -417,6 +421,123 @@ def windowed_fa(q, k, v, windowsize: int, stride: Optional[int] = None,
                               nsp, spa, d, dv, B, windowsize, stride, pad,
                               float(scale), _ptr(ws), int(nws), _stream(q)))
     return y, lw, mw
+
+
+def _window_args(spatial, windowsize, stride, pad):
+    stride = windowsize if stride is None else int(stride)
+    pad = (windowsize - 1) // 2 if pad is None else int(pad)
+    nsp = len(spatial)
+    _require(1 <= nsp <= 3, "1 to 3 spatial dims supported")
+    outs = window_geometry(spatial, windowsize, stride, pad)
+    return stride, pad, nsp, outs
+
+
+def window(x: torch.Tensor, windowsize: int, stride: Optional[int] = None,
+           pad: Optional[int] = None) -> torch.Tensor:
+    """``window(x, ws; stride=ws, pad=(ws-1)÷2)`` — src/utils.jl:36-45
+    (NNlib.unfold) on the device: x (S..., C, B) -> (ws^k, C, L, B), zero padding."""
+    D = x.dim()
+    _require(D >= 3, "x must have rank >= 3: (spatial..., C, B)")
+    sp = tuple(x.shape[:D - 2])
+    C, B = x.shape[D - 2], x.shape[D - 1]
+    stride, pad, nsp, outs = _window_args(sp, windowsize, stride, pad)
+    code = _dtype_code(x)
+    _device_check(x)
+    X = jl_empty((windowsize ** nsp, C, math.prod(outs), B), x.dtype, x.device)
+    _check(lib().fa_window(code, _ptr(x), _ptr(X), nsp, _i64_array(sp), C, B, windowsize, stride, pad,
+                           _stream(x)))
+    return X
+
+
+def unwindow(X: torch.Tensor, outputsize: Sequence[int], windowsize: int, stride: Optional[int] = None,
+             pad: Optional[int] = None) -> torch.Tensor:
+    """``unwindow(X, outputsize, ws; stride, pad)`` — src/utils.jl:47-54
+    (NNlib.fold): (ws^k, C, L, B) -> outputsize = (S..., C, B), overlapping
+    window contributions SUMMED (0 where no window covers a pixel)."""
+    outputsize = tuple(int(o) for o in outputsize)
+    _require(len(outputsize) >= 3 and X.dim() == 4, "X: (ws^k, C, L, B); outputsize: (spatial..., C, B)")
+    sp = outputsize[:-2]
+    C, B = outputsize[-2], outputsize[-1]
+    stride, pad, nsp, outs = _window_args(sp, windowsize, stride, pad)
+    _require(tuple(X.shape) == (windowsize ** nsp, C, math.prod(outs), B),
+             f"X has shape {tuple(X.shape)}, the geometry needs {(windowsize ** nsp, C, math.prod(outs), B)}")
+    code = _dtype_code(X)
+    _device_check(X)
+    x = jl_empty(outputsize, X.dtype, X.device)
+    _check(lib().fa_unwindow(code, _ptr(X), _ptr(x), nsp, _i64_array(sp), C, B, windowsize, stride, pad,
+                             _stream(X)))
+    return x
+
+
+def _rm(t: torch.Tensor) -> torch.Tensor:
+    """Row-major view (reversed dims) of a Julia column-major tensor: same memory."""
+    return t.permute(*range(t.dim() - 1, -1, -1))
+
+
+def jl_reshape(t: torch.Tensor, shape: Sequence[int]) -> torch.Tensor:
+    """Julia ``reshape`` (column-major order) of a column-major contiguous tensor: a view."""
+    _require(is_jl_contiguous(t), "jl_reshape needs a Julia column-major contiguous tensor")
+    return _rm(_rm(t).reshape(tuple(int(x) for x in reversed(tuple(shape)))))
+
+
+def dense_dpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float = 0.0):
+    """``dense_dpa(q, k, v) -> (y, P)`` — src/naive/dense.jl:1-35, the reference's
+    materialising attention (its test oracle for dense_fa, test/test.jl:19):
+    P = softmax(τ Q Kᵀ; dims=2) as an (N, Nk, B) array, y = P V.
+
+    The two products are plain library GEMMs (hipBLASLt through torch.bmm on
+    the column-major views; no transpose copies), the softmax is this
+    library's fa_softmax kernel (dims = 2).  P is in the input dtype, as the
+    reference computes it in T.  Memory is O(N·Nk·B): use dense_fa for size."""
+    D = q.dim()
+    _require(D >= 3 and k.dim() == D and v.dim() == D, "q, k, v must share rank >= 3")
+    dqk, B = q.shape[D - 2], q.shape[D - 1]
+    dvo = v.shape[D - 2]
+    _require(k.shape[D - 2] == dqk and k.shape[D - 1] == B and v.shape[D - 1] == B,
+             "DimensionMismatch: k must match q's feature and batch dims, v the batch dim")
+    _dtype_code(q, k, v)
+    _device_check(q, k, v)
+    _require(all(is_jl_contiguous(t) for t in (q, k, v)), "q, k, v must be Julia column-major contiguous")
+    N = math.prod(q.shape[:D - 2])
+    Nk = math.prod(k.shape[:D - 2])
+    _require(math.prod(v.shape[:D - 2]) == Nk, "DimensionMismatch: v must have k's token count")
+    tau = float(scale) if scale > 0 else 1.0 / math.sqrt(dqk)
+    Qr = _rm(q).reshape(B, dqk, N)           # column-major (N, d, B) = row-major [B][d][N]
+    Kr = _rm(k).reshape(B, dqk, Nk)
+    Vr = _rm(v).reshape(B, dvo, Nk)
+    St = torch.bmm(Kr.transpose(1, 2), Qr)  # [B][Nk][N] = column-major (N, Nk, B): P's layout
+    St.mul_(tau)
+    P = _rm(St)                               # (N, Nk, B) view
+    fused_softmax_(P, P, dims=2)
+    Y = torch.bmm(Vr, St)                     # [B][dv][N] = column-major (N, dv, B)
+    y = jl_reshape(_rm(Y), tuple(q.shape[:D - 2]) + (dvo, B))
+    return y, P
+
+
+def windowed_dpa(q, k, v, windowsize: int, stride: Optional[int] = None, pad: Optional[int] = None):
+    """``windowed_dpa(q, k, v, ws; stride, pad) -> (y, P)`` — src/naive/windowed.jl:3-22:
+    window (fa_window) → dense_dpa over the (ws^k, d, L·B) window batch →
+    unwindow (fa_unwindow) ÷ coverage (unwindow of windowed ones, :16-17).
+    P: (ws^k, ws^k, L, B).  Uncovered pixels are 0/0 = NaN, as the reference."""
+    D = q.dim()
+    sp = tuple(q.shape[:D - 2])
+    dvo, B = v.shape[D - 2], v.shape[D - 1]
+    stride, pad, nsp, outs = _window_args(sp, windowsize, stride, pad)
+    qw, kw, vw = (window(a, windowsize, stride, pad) for a in (q, k, v))
+    T, L = windowsize ** nsp, math.prod(outs)
+    yw, Pw = dense_dpa(*(jl_reshape(a, (T, a.shape[1], L * B)) for a in (qw, kw, vw)))
+    szy = sp + (dvo, B)
+    ones = jl_empty(szy, v.dtype, v.device).fill_(1)
+    divisor = unwindow(window(ones, windowsize, stride, pad), szy, windowsize, stride, pad)
+    y = unwindow(jl_reshape(yw, (T, dvo, L, B)), szy, windowsize, stride, pad)
+    y.div_(divisor)
+    return y, jl_reshape(Pw, (T, T, L, B))
+
+
+def block_dpa(q, k, v, windowsize: int):
+    """``block_dpa(q, k, v, ws) = windowed_dpa(q, k, v, ws)`` — src/naive/windowed.jl:1
+    (the reference passes no keywords: stride = ws, pad = (ws-1)÷2)."""
+    return windowed_dpa(q, k, v, windowsize)
 
 
 def block_fa(q, k, v, windowsize: int, pad: int = 0, scale: float = 0.0):

@@ -126,6 +126,31 @@ function windowed_fa_backward(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,
     return dq, dk, dv_
 end
 
+# window(x, ws; stride, pad) / unwindow(X, size(x), ws; stride, pad) — src/utils.jl:36-54
+# (NNlib.unfold / NNlib.fold, the sum over overlapping windows) on the device
+function window(x::ROCArray{T,N}, windowsize; stride=windowsize, pad=(windowsize - 1) ÷ 2) where {T,N}
+    nsp = N - 2
+    spatial = Int64[size(x, i) for i in 1:nsp]
+    C, B = size(x, N - 1), size(x, N)
+    L = prod((s + 2pad - windowsize) ÷ stride + 1 for s in spatial)
+    X = similar(x, windowsize^nsp, C, L, B)
+    fa_check(ccall((:fa_window, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Ptr{Cvoid}),
+                   fa_dtype(T), x, X, nsp, spatial, C, B, windowsize, stride, pad, stream_ptr()))
+    return X
+end
+function unwindow(X::ROCArray{T,4}, outputsize::NTuple{N}, windowsize;
+                  stride=windowsize, pad=(windowsize - 1) ÷ 2) where {T,N}
+    nsp = N - 2
+    spatial = Int64[outputsize[i] for i in 1:nsp]
+    C, B = size(X, 2), size(X, 4)
+    x = similar(X, outputsize...)
+    fa_check(ccall((:fa_unwindow, libfa_hip), Cint,
+                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Ptr{Cvoid}),
+                   fa_dtype(T), X, x, nsp, spatial, C, B, windowsize, stride, pad, stream_ptr()))
+    return x
+end
+
 fa_abi_version() = ccall((:fa_abi_version, libfa_hip), Cint, ())
 fa_max_head_dim() = ccall((:fa_max_head_dim, libfa_hip), Cint, ())
 

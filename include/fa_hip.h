@@ -110,6 +110,21 @@ size_t fa_windowed_fwd_workspace(int dtype, int nspatial, const int64_t* spatial
                                  int64_t d, int64_t dv, int64_t batch,
                                  int64_t ws, int64_t stride, int64_t pad);
 
+/* window(x, ws; stride, pad) — reference src/utils.jl:36-45 (NNlib.unfold):
+ * x (S_1..S_k, C, batch) -> xw (ws^k, C, L, batch), zero padding outside the
+ * image, window token order first-spatial-dim fastest.  xw fully written. */
+int fa_window(int dtype, const void* x, void* xw,
+              int nspatial, const int64_t* spatial, int64_t C, int64_t batch,
+              int64_t ws, int64_t stride, int64_t pad, void* hip_stream);
+
+/* unwindow(xw, size(x), ws; stride, pad) — reference src/utils.jl:47-54
+ * (NNlib.fold): xw (ws^k, C, L, batch) -> x (S_1..S_k, C, batch), the SUM over
+ * overlapping windows (0 where no window covers a pixel).  Deterministic (one
+ * thread per output pixel, fixed window order).  x fully written. */
+int fa_unwindow(int dtype, const void* xw, void* x,
+                int nspatial, const int64_t* spatial, int64_t C, int64_t batch,
+                int64_t ws, int64_t stride, int64_t pad, void* hip_stream);
+
 /* Workspace bytes fa_windowed_bwd needs. */
 size_t fa_windowed_workspace(int dtype, int nspatial, const int64_t* spatial,
                              int64_t d, int64_t dv, int64_t batch,
