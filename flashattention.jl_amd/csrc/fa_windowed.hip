@@ -916,6 +916,221 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
     FA_STAMP(5);
 }
 
+// --------------------------------------------------------------------------
+// Fused windowed BACKWARD, one window per workgroup (bf16/f16, 2-D, stride >= ws,
+// ws <= 7, d, dv <= 64): the exact chain rule of windowed_fa for non-overlapping
+// windows, where every covered pixel belongs to exactly one window, so
+// dyw = window(dy ./ count) is dy itself and the fold is a direct store.
+// Replaces, for these shapes, the composed gather -> dense backward -> fold
+// path (T = 49 tokens is not a multiple of 8, so that path runs the SIMT
+// backward: 20 ms at B = 32).
+//
+//   staging  : q, k, v, dy rows by the row-shift loads of the forward kernel into
+//              [feature][slot] images (128-B swizzled rows); y rows only feed
+//              D = rowsum(dy ∘ y), accumulated per slot with LDS float adds.
+//   phase 1  : wave (qb, kb) computes the 32x32 blocks S = Q Kᵀ and dP = dO Vᵀ
+//              (queries on accumulator rows, keys on lanes) with −lse/τ and −D as
+//              the initial accumulators, P = exp2(c·S'), dS = P ∘ (dP − D), and
+//              writes P, dS (bf16) into [key][query] images (144-B rows).
+//   phase 2  : 12 blocks over the 4 waves: dVᵀ = dOᵀ P, dKᵀ = τ Qᵀ dS (row
+//              reads), dQᵀ = τ Kᵀ dSᵀ (dSᵀ by transposed reads of the [key][query]
+//              image); each lane stores one slot's features straight to its pixel.
+// Padding slots (tx or ty >= ws): keys masked (P = dS = 0), queries have lse = +inf.
+// --------------------------------------------------------------------------
+template <class T, int D, int DV>
+__global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, const T* __restrict__ k,
+                                                    const T* __restrict__ v, const T* __restrict__ y,
+                                                    const T* __restrict__ dy, const float* __restrict__ lw,
+                                                    const float* __restrict__ mw, T* __restrict__ dq,
+                                                    T* __restrict__ dk, T* __restrict__ dvo, WinDev g, int d,
+                                                    int dv, float scale, float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int NTH = 256, KROW = 128, PROW = 144;
+    constexpr int QIMG = D * KROW, VIMG = DV * KROW, PIMG = 64 * PROW;
+    constexpr int OQ = 0, OK_ = QIMG, OV = 2 * QIMG, ODO = 2 * QIMG + VIMG, OP = 2 * QIMG + 2 * VIMG,
+                  ODS = OP + PIMG, OLSE = ODS + PIMG, OD = OLSE + 256, REGION = OD + 256;
+    constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;
+    static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
+    __shared__ __attribute__((aligned(16))) char smem[REGION];
+    auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
+    float* const lse_s = (float*)(smem + OLSE);   // −lse/τ per query slot (raw score units)
+    float* const dsum = (float*)(smem + OD);      // D per query slot
+
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
+    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
+    const int ax = min(max(xs & ~1, 0), W_ - 8);
+    const int sh = xs - ax;
+    const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+
+    auto item_off = [&](int it, int C) {
+        const int yy = it & 7, f = it >> 3, yr = y0 + yy;
+        const bool ok = yy < ws && yr >= 0 && yr < H_ && f < C;
+        return ok ? (f * P_ + yr * W_ + ax) * 2 : 0x7FFFFFF0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    const auto yrs = slab_rsrc(y + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    const auto drs = slab_rsrc(dy + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    u32x4 rq[NIQ], rk[NIQ], rv[NIV], ry[NIV], rd[NIV];
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        const int o = item_off(tid + NTH * j, d);
+        rq[j] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o, 0, 0);
+        rk[j] = __builtin_amdgcn_raw_buffer_load_b128(krs, o, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int o = item_off(tid + NTH * j, dv);
+        rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, o, 0, 0);
+        rd[j] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
+        ry[j] = __builtin_amdgcn_raw_buffer_load_b128(yrs, o, 0, 0);
+    }
+    // per-slot constants: −lse/τ (+inf lse outside the window) and D = 0
+    if (tid < 64) {
+        const int tx = tid & 7, ty = tid >> 3;
+        float nl = kNegInf;
+        if (tx < ws && ty < ws) {
+            const int64_t li = ty * ws + tx + (int64_t)g.T * wid;
+            nl = -(mw[li] + __logf(lw[li])) / scale;
+        }
+        lse_s[tid] = nl;
+        dsum[tid] = 0.0f;
+    }
+    unsigned mask[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int t0 = 2 * j, t1 = 2 * j + 1;
+        const bool v0 = t0 < ws && xs + t0 >= 0 && xs + t0 < W_;
+        const bool v1 = t1 < ws && xs + t1 >= 0 && xs + t1 < W_;
+        mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
+    }
+    auto koff = [&](int it) {
+        const int yy = it & 7, f = it >> 3;
+        return f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
+    };
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        const int o = koff(tid + NTH * j);
+        *(u32x4*)(smem + OQ + o) = shift_row(rq[j], sh, mask);
+        *(u32x4*)(smem + OK_ + o) = shift_row(rk[j], sh, mask);
+    }
+    lds_barrier();   // dsum zeroed before the adds below
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int it = tid + NTH * j, o = koff(it), yy = it & 7;
+        const u32x4 dd = shift_row(rd[j], sh, mask), yv = shift_row(ry[j], sh, mask);
+        *(u32x4*)(smem + OV + o) = shift_row(rv[j], sh, mask);
+        *(u32x4*)(smem + ODO + o) = dd;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const unsigned short a16 = (unsigned short)((e & 1) ? (dd[e >> 1] >> 16) : (dd[e >> 1] & 0xFFFFu));
+            const unsigned short b16 = (unsigned short)((e & 1) ? (yv[e >> 1] >> 16) : (yv[e >> 1] & 0xFFFFu));
+            const float pr = (float)__builtin_bit_cast(T, a16) * (float)__builtin_bit_cast(T, b16);
+            if (pr != 0.0f) atomicAdd(&dsum[yy * 8 + e], pr);
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 1: S and dP blocks (qb, kb) of this wave ----
+    const int qb = wave & 1, kb = wave >> 1;
+    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    // tr-read of a [feature][slot] image: 32 slots of block sb, features 16 s + 8 h .. + 7
+    auto frag_tr = [&](int img, int sb, int s16) {
+        const int orow = (16 * s16 + 8 * h + qq) * KROW;
+        const char* a = smem + img + orow + (((sb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
+        return __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                       __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    f32x16 sa, pa;
+#pragma unroll
+    for (int x4 = 0; x4 < 4; ++x4) {
+        const int qrow = qb * 32 + acc_row(4 * x4, h);
+        const f32x4 l4 = *(const f32x4*)(lse_s + qrow);
+        const f32x4 d4 = *(const f32x4*)(dsum + qrow);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { sa[4 * x4 + e] = l4[e]; pa[4 * x4 + e] = -d4[e]; }
+    }
+#pragma unroll
+    for (int s16 = 0; s16 < D / 16; ++s16) sa = mfma32x32x16(frag_tr(OQ, qb, s16), frag_tr(OK_, kb, s16), sa);
+#pragma unroll
+    for (int s16 = 0; s16 < DV / 16; ++s16) pa = mfma32x32x16(frag_tr(ODO, qb, s16), frag_tr(OV, kb, s16), pa);
+    const int kslot = kb * 32 + r;
+    const bool kvalid = (kslot & 7) < ws && (kslot >> 3) < ws;
+    // P and dS into [key][query] images, 4 consecutive queries per 8-byte write
+#pragma unroll
+    for (int x4 = 0; x4 < 4; ++x4) {
+        typename Frag8<T>::half p4, s4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float pr = kvalid ? exp2_fast(sa[4 * x4 + e] * scale_log2) : 0.0f;
+            p4[e] = (T)pr;
+            s4[e] = (T)(pr * pa[4 * x4 + e]);
+        }
+        const int o = kslot * PROW + (qb * 32 + acc_row(4 * x4, h)) * 2;
+        *(typename Frag8<T>::half*)(smem + OP + o) = p4;
+        *(typename Frag8<T>::half*)(smem + ODS + o) = s4;
+    }
+    lds_barrier();
+
+    // ---- phase 2: dVᵀ, dKᵀ, dQᵀ blocks ----
+    // row read: 8 consecutive slots 16 s + 8 h of feature row f of a [feature][slot] image
+    auto frag_row = [&](int img, int f, int s16) {
+        return *(const F8*)(smem + img + f * KROW + ((s16 ^ kswz(f)) * 32) + 16 * h);
+    };
+    auto store_px = [&](T* out, int C, int slot, int fbase, const f32x16& acc, float mul) {
+        const int tx = slot & 7, ty = slot >> 3, px = xs + tx, py = y0 + ty;
+        if (tx < ws && ty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+            T* ob = out + (int64_t)b * C * P_ + (int64_t)py * W_ + px;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int f = fbase + acc_row(x, h);
+                if (f < C) ob[(int64_t)f * P_] = (T)(acc[x] * mul);
+            }
+        }
+    };
+    constexpr int NDV = DV / 32 * 2, NDK = D / 32 * 2, NBLK = NDV + 2 * NDK;
+#pragma unroll
+    for (int i = 0; i < (NBLK + 3) / 4; ++i) {
+        const int blk = wave + 4 * i;
+        if (blk >= NBLK) break;
+        f32x16 acc;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
+        if (blk < NDV) {                              // dVᵀ[cb, kb2] = dOᵀ P
+            const int cb = blk >> 1, kb2 = blk & 1, f = cb * 32 + r;
+#pragma unroll
+            for (int s16 = 0; s16 < 4; ++s16)
+                acc = mfma32x32x16(frag_row(ODO, f, s16),
+                                   *(const F8*)(smem + OP + (kb2 * 32 + r) * PROW + (16 * s16 + 8 * h) * 2), acc);
+            store_px(dvo, dv, kb2 * 32 + r, cb * 32, acc, 1.0f);
+        } else if (blk < NDV + NDK) {                 // dKᵀ[fb, kb2] = τ Qᵀ dS
+            const int b2 = blk - NDV, fb = b2 >> 1, kb2 = b2 & 1, f = fb * 32 + r;
+#pragma unroll
+            for (int s16 = 0; s16 < 4; ++s16)
+                acc = mfma32x32x16(frag_row(OQ, f, s16),
+                                   *(const F8*)(smem + ODS + (kb2 * 32 + r) * PROW + (16 * s16 + 8 * h) * 2), acc);
+            store_px(dk, d, kb2 * 32 + r, fb * 32, acc, scale);
+        } else {                                      // dQᵀ[fb, qb2] = τ Kᵀ dSᵀ
+            const int b2 = blk - NDV - NDK, fb = b2 >> 1, qb2 = b2 & 1, f = fb * 32 + r;
+#pragma unroll
+            for (int s16 = 0; s16 < 4; ++s16) {
+                const char* a = smem + ODS + (16 * s16 + 8 * h + qq) * PROW + (qb2 * 32 + kh * 16 + 4 * pp) * 2;
+                const F8 bt = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                                      __builtin_bit_cast(F4, ds_read_tr16(a + 4 * PROW)),
+                                                      0, 1, 2, 3, 4, 5, 6, 7);
+                acc = mfma32x32x16(frag_row(OK_, f, s16), bt, acc);
+            }
+            store_px(dq, d, qb2 * 32 + r, fb * 32, acc, scale);
+        }
+    }
+}
+
 int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default)
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
@@ -1196,6 +1411,42 @@ static int windowed_bwd_typed(const WindowedBwdArgs& a, hipStream_t s, const cha
     return FA_OK;
 }
 
+// fused windowed backward eligibility (the row-shift forward's shapes)
+static bool bwd_rows_ok(const WindowedBwdArgs& a) {
+    const bool al = ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 && ((uintptr_t)a.v & 15u) == 0 &&
+                    ((uintptr_t)a.y & 15u) == 0 && ((uintptr_t)a.dy & 15u) == 0;
+    return g_win_force_composed != 1 && a.dtype != FA_DTYPE_F32 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
+           a.g.ws <= 7 && a.g.S[0] % 8 == 0 && a.d <= 64 && a.dv <= 64 && al &&
+           a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX;
+}
+
+template <class T>
+static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
+    const WinDev g = to_dev(a.g);
+    hipError_t e = hipSuccess;
+    if (!fully_covered(a.g)) {   // pixels no window covers get zero gradient
+        if ((e = hipMemsetAsync(a.dq, 0, (size_t)(a.g.P * a.d * a.batch) * sizeof(T), s)) != hipSuccess ||
+            (e = hipMemsetAsync(a.dk, 0, (size_t)(a.g.P * a.d * a.batch) * sizeof(T), s)) != hipSuccess ||
+            (e = hipMemsetAsync(a.dv_, 0, (size_t)(a.g.P * a.dv * a.batch) * sizeof(T), s)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
+    }
+    const dim3 grid((unsigned)(a.g.L * a.batch));
+#define FA_BWD_ROWS(DD, DVV)                                                                                 hipLaunchKernelGGL((win_bwd_rows<T, DD, DVV>), grid, dim3(256), 0, s, (const T*)a.q, (const T*)a.k,                         (const T*)a.v, (const T*)a.y, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk,                              (T*)a.dv_, g, (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e)
+    const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
+    if (Dc == 32 && DVc == 32) FA_BWD_ROWS(32, 32);
+    else if (Dc == 32) FA_BWD_ROWS(32, 64);
+    else if (DVc == 32) FA_BWD_ROWS(64, 32);
+    else FA_BWD_ROWS(64, 64);
+#undef FA_BWD_ROWS
+    if ((e = hipGetLastError()) != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return FA_ERR_HIP;
+    }
+    return FA_OK;
+}
+
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
         *why = "head dimension exceeds the compiled maximum (128)";
@@ -1204,6 +1455,12 @@ int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** wh
     if (!geom_fits(a.g, a.d, a.dv, a.batch)) {
         *why = "windowed problem too large for 32-bit window indexing";
         return FA_ERR_UNSUPPORTED;
+    }
+    if (bwd_rows_ok(a)) {
+        switch (a.dtype) {
+            case FA_DTYPE_BF16: return windowed_bwd_rows<bf16>(a, s, why);
+            case FA_DTYPE_F16: return windowed_bwd_rows<f16>(a, s, why);
+        }
     }
     switch (a.dtype) {
         case FA_DTYPE_BF16: return windowed_bwd_typed<bf16>(a, s, why);

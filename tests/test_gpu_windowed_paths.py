@@ -67,3 +67,35 @@ def test_windowed_forced_path(fa, geom, path):
             assert_lm_close(_np(m), mr, "bfloat16", f"m ({tag})")
     finally:
         L.fa_debug_set_win_composed(old)
+
+
+BWD_GEOMS = [g for g in GEOMS if g[3] >= g[2] and g[2] <= 7]   # stride >= ws, ws <= 7: the fused backward
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("geom", BWD_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_backward_paths(fa, geom, path):
+    """Fused windowed backward (path 0: win_bwd_rows) and the composed
+    gather → dense backward → fold path (1) vs the oracle chain rule."""
+    W, H, ws, st, pad = geom
+    rng = np.random.default_rng(W * 7 + H * 3 + ws)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        for (d, dv) in DIMS:
+            B = 2
+            q, k = (bf(rng.standard_normal((W, H, d, B))) for _ in range(2))
+            v, dy = (bf(rng.standard_normal((W, H, dv, B))) for _ in range(2))
+            Q, K, V, DY = (fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v, dy))
+            y, l, m = fa.windowed_fa(Q, K, V, ws, stride=st, pad=pad)
+            dq, dk, dvv = fa.windowed_fa_backward(Q, K, V, y, DY, l, m, ws, stride=st, pad=pad)
+            torch.cuda.synchronize()
+            ref = O.windowed_fa_backward(q, k, v, dy, ws, st, pad)
+            for a, b_, nm in zip((dq, dk, dvv), ref, ("dq", "dk", "dv")):
+                x = _np(a)
+                scale = max(np.abs(b_).max(), 1e-2)
+                err = np.abs(x - b_).max() / scale
+                assert np.all(np.isfinite(x)) and err <= 2e-2, f"path {path} d {d} dv {dv} {nm}: {err:.2e}"
+    finally:
+        L.fa_debug_set_win_composed(old)
