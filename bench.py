@@ -248,6 +248,13 @@ def extra_benches(fa_hip, args, dist):
             bytes_alg = Bimg * (3 * 128 * 128 * 64 * 2 + 128 * 128 * 64 * 2 + 2 * T * L * 4)
             res[f"cfg3_windowed_B{Bimg}_GBs"] = bytes_alg / t / 1e9
             res[f"cfg3_windowed_B{Bimg}_us"] = t * 1e6
+            # backward of the same shape: q, k, v, y, dy read, dq, dk, dv written
+            dy = _randn_jl(fa_hip, (128, 128, 64, Bimg), torch.bfloat16, gen)
+            y, lw, mw = fa_hip.windowed_fa(q, k, v, 7)
+            tb = time_graph(lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), max(5, args.steps // 4), dist)
+            bytes_bwd = Bimg * (8 * 128 * 128 * 64 * 2 + 2 * T * L * 4)
+            res[f"cfg3_windowed_bwd_B{Bimg}_GBs"] = bytes_bwd / tb / 1e9
+            res[f"cfg3_windowed_bwd_B{Bimg}_us"] = tb * 1e6
         except fa_hip.FlashAttentionError as ex:
             res[f"cfg3_windowed_B{Bimg}"] = str(ex)
     # circulant: the reference's runcirculant shape
