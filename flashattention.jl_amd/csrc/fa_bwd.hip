@@ -565,8 +565,99 @@ static hipError_t launch_fast(const BwdParams& p, hipStream_t s) {
 // --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
-size_t dense_bwd_workspace(int, int64_t N, int64_t, int64_t, int64_t, int64_t batch) {
-    return (size_t)(2 * N * batch * sizeof(float) + 256);
+// --------------------------------------------------------------------------
+// Padded fast path: 16-bit shapes the MFMA kernels do not take directly (N or
+// Nk not a multiple of 8, d or dv not 32 / 64 / 128) are copied into zero-padded
+// workspace slabs (N -> N8, Nk -> Nk8, d, dv -> their class) and run on the fast
+// kernels.  Zero keys and values are exact there: with the forward's lse they add
+// P·0 to dP and dS·0 to dQ, and their own dK / dV rows are dropped; padded
+// queries carry dO = O = 0 (so dS = 0) and l = 1, m = 0 (finite P, no NaN).
+// --------------------------------------------------------------------------
+static bool cls_dim(int64_t x) { return x == 32 || x == 64 || x == 128; }
+static bool shape_fast(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv) {
+    return dtype != FA_DTYPE_F32 && cls_dim(d) && cls_dim(dv) && N % 8 == 0 && Nk % 8 == 0 &&
+           N * d * 2 < INT32_MAX && Nk * d * 2 < INT32_MAX && N * dv * 2 < INT32_MAX && Nk * dv * 2 < INT32_MAX;
+}
+struct BwdPad {
+    bool on = false;
+    int64_t Np = 0, Nkp = 0, Dp = 0, DVp = 0;
+    size_t bytes = 0;
+};
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    BwdPad pl;
+    if (dtype == FA_DTYPE_F32 || d > kMaxHeadDim || dv > kMaxHeadDim || shape_fast(dtype, N, Nk, d, dv)) return pl;
+    pl.Np = (N + 7) / 8 * 8;
+    pl.Nkp = (Nk + 7) / 8 * 8;
+    pl.Dp = head_dim_class(d);
+    pl.DVp = head_dim_class(dv);
+    if (!shape_fast(dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp) || pl.Np * batch > INT32_MAX / 2 ||
+        pl.Nkp * batch > INT32_MAX / 2)
+        return pl;
+    pl.on = true;
+    const size_t q = al256((size_t)(pl.Np * pl.Dp * batch) * 2), k = al256((size_t)(pl.Nkp * pl.Dp * batch) * 2);
+    const size_t v = al256((size_t)(pl.Nkp * pl.DVp * batch) * 2), o = al256((size_t)(pl.Np * pl.DVp * batch) * 2);
+    const size_t lm = al256((size_t)(pl.Np * batch) * 4);
+    pl.bytes = 2 * q + 2 * k + 2 * v + 2 * o + 2 * lm;   // Q dQ, K dK, V dV, O dO, l m
+    return pl;
+}
+
+size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    const BwdPad pl = pad_plan(dtype, N, Nk, d, dv, batch);
+    const int64_t rows = pl.on ? pl.Np : N;
+    return (size_t)(2 * rows * batch * sizeof(float) + 256) + (pl.on ? pl.bytes + 256 : 0);
+}
+
+// dst (Np, Cp, B) <- src (N, C, B), zero-filled
+template <class T>
+__global__ __launch_bounds__(256) void bwd_pad(const T* __restrict__ src, T* __restrict__ dst, int N, int C,
+                                               int Np, int Cp, int64_t total) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int n = (int)(e % Np);
+    const int64_t bc = e / Np;
+    const int c = (int)(bc % Cp);
+    const int64_t b = bc / Cp;
+    dst[e] = (n < N && c < C) ? src[(b * C + c) * N + n] : (T)0.0f;
+}
+// dst (N, C, B) <- src (Np, Cp, B)
+template <class T>
+__global__ __launch_bounds__(256) void bwd_unpad(const T* __restrict__ src, T* __restrict__ dst, int N, int C,
+                                                 int Np, int Cp, int64_t total) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int n = (int)(e % N);
+    const int64_t bc = e / N;
+    const int c = (int)(bc % C);
+    const int64_t b = bc / C;
+    dst[e] = src[(b * Cp + c) * Np + n];
+}
+// l, m (N, 1, B) -> (Np, 1, B); padded queries get l = 1, m = 0
+__global__ __launch_bounds__(256) void bwd_pad_lm(const float* __restrict__ l, const float* __restrict__ m,
+                                                  float* __restrict__ lp, float* __restrict__ mp, int N, int Np,
+                                                  int64_t total) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int n = (int)(e % Np);
+    const int64_t b = e / Np;
+    lp[e] = n < N ? l[b * N + n] : 1.0f;
+    mp[e] = n < N ? m[b * N + n] : 0.0f;
+}
+template <class T>
+static hipError_t pad_launch(const void* src, void* dst, int64_t N, int64_t C, int64_t Np, int64_t Cp, int64_t B,
+                             hipStream_t s) {
+    const int64_t total = Np * Cp * B;
+    hipLaunchKernelGGL(bwd_pad<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const T*)src, (T*)dst,
+                       (int)N, (int)C, (int)Np, (int)Cp, total);
+    return hipGetLastError();
+}
+template <class T>
+static hipError_t unpad_launch(const void* src, void* dst, int64_t N, int64_t C, int64_t Np, int64_t Cp, int64_t B,
+                               hipStream_t s) {
+    const int64_t total = N * C * B;
+    hipLaunchKernelGGL(bwd_unpad<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const T*)src, (T*)dst,
+                       (int)N, (int)C, (int)Np, (int)Cp, total);
+    return hipGetLastError();
 }
 
 template <class T>
@@ -616,12 +707,62 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     p.N = (int)a.N; p.Nk = (int)a.Nk; p.d = (int)a.d; p.dv = (int)a.dv; p.batch = (int)a.batch;
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
-    auto cls = [](int64_t x) { return x == 32 || x == 64 || x == 128; };
-    const bool fast = !g_bwd_force_generic && a.dtype != FA_DTYPE_F32 && cls(a.d) && cls(a.dv) &&
-                      a.N % 8 == 0 && a.Nk % 8 == 0 && a.N * a.d * 2 < INT32_MAX &&
-                      a.Nk * a.d * 2 < INT32_MAX && a.N * a.dv * 2 < INT32_MAX && a.Nk * a.dv * 2 < INT32_MAX &&
+    const bool fast = !g_bwd_force_generic && shape_fast(a.dtype, a.N, a.Nk, a.d, a.dv) &&
                       aligned16(a.Q) && aligned16(a.K) && aligned16(a.V) && aligned16(a.dO);
+    const BwdPad pl = pad_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
     hipError_t e;
+    if (!fast && pl.on && !g_bwd_force_generic) {
+        // padded fast path: workspace = [nD | nlse] (Np rows) then the padded slabs
+        const int64_t B = a.batch;
+        char* w = (char*)(ws + al256((size_t)(2 * pl.Np * B) * sizeof(float)));
+        auto take = [&](size_t bytes) { void* q = w; w += al256(bytes); return q; };
+        void* Qp = take((size_t)(pl.Np * pl.Dp * B) * 2);
+        void* dQp = take((size_t)(pl.Np * pl.Dp * B) * 2);
+        void* Kp = take((size_t)(pl.Nkp * pl.Dp * B) * 2);
+        void* dKp = take((size_t)(pl.Nkp * pl.Dp * B) * 2);
+        void* Vp = take((size_t)(pl.Nkp * pl.DVp * B) * 2);
+        void* dVp = take((size_t)(pl.Nkp * pl.DVp * B) * 2);
+        void* Op = take((size_t)(pl.Np * pl.DVp * B) * 2);
+        void* dOp = take((size_t)(pl.Np * pl.DVp * B) * 2);
+        float* lp = (float*)take((size_t)(pl.Np * B) * 4);
+        float* mp = (float*)take((size_t)(pl.Np * B) * 4);
+        if ((size_t)(w - (char*)a.workspace) > a.workspace_bytes) {
+            *why = "workspace smaller than fa_dense_bwd_workspace()";
+            return FA_ERR_WORKSPACE;
+        }
+        const bool half = a.dtype == FA_DTYPE_F16;
+        auto pad = [&](const void* src, void* dst, int64_t N, int64_t C, int64_t Np, int64_t Cp) {
+            return half ? pad_launch<f16>(src, dst, N, C, Np, Cp, B, s) : pad_launch<bf16>(src, dst, N, C, Np, Cp, B, s);
+        };
+        auto unpad = [&](const void* src, void* dst, int64_t N, int64_t C, int64_t Np, int64_t Cp) {
+            return half ? unpad_launch<f16>(src, dst, N, C, Np, Cp, B, s) : unpad_launch<bf16>(src, dst, N, C, Np, Cp, B, s);
+        };
+        const int64_t tlm = pl.Np * B;
+        if ((e = pad(a.Q, Qp, a.N, a.d, pl.Np, pl.Dp)) != hipSuccess ||
+            (e = pad(a.K, Kp, a.Nk, a.d, pl.Nkp, pl.Dp)) != hipSuccess ||
+            (e = pad(a.V, Vp, a.Nk, a.dv, pl.Nkp, pl.DVp)) != hipSuccess ||
+            (e = pad(a.O, Op, a.N, a.dv, pl.Np, pl.DVp)) != hipSuccess ||
+            (e = pad(a.dO, dOp, a.N, a.dv, pl.Np, pl.DVp)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
+        hipLaunchKernelGGL(bwd_pad_lm, dim3((unsigned)((tlm + 255) / 256)), dim3(256), 0, s, a.l, a.m, lp, mp,
+                           (int)a.N, (int)pl.Np, tlm);
+        BwdParams q = p;
+        q.Q = Qp; q.K = Kp; q.V = Vp; q.O = Op; q.dO = dOp; q.l = lp; q.m = mp;
+        q.dQ = dQp; q.dK = dKp; q.dV = dVp;
+        q.nlse = q.nD + pl.Np * B;
+        q.N = (int)pl.Np; q.Nk = (int)pl.Nkp; q.d = (int)pl.Dp; q.dv = (int)pl.DVp;
+        e = half ? launch_typed<f16>(q, s, true) : launch_typed<bf16>(q, s, true);
+        if (e == hipSuccess && (e = unpad(dQp, a.dQ, a.N, a.d, pl.Np, pl.Dp)) == hipSuccess &&
+            (e = unpad(dKp, a.dK, a.Nk, a.d, pl.Nkp, pl.Dp)) == hipSuccess)
+            e = unpad(dVp, a.dV, a.Nk, a.dv, pl.Nkp, pl.DVp);
+        if (e != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
+        return FA_OK;
+    }
     switch (a.dtype) {
         case FA_DTYPE_BF16: e = launch_typed<bf16>(p, s, fast); break;
         case FA_DTYPE_F16: e = launch_typed<f16>(p, s, fast); break;

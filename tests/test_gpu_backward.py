@@ -152,3 +152,32 @@ def test_backward_head_dim_sweep(fa, d, dv):
     assert_grad_close(dq, dqr, "bfloat16", "dQ")
     assert_grad_close(dk, dkr, "bfloat16", "dK")
     assert_grad_close(dv_, dvr, "bfloat16", "dV")
+
+
+@pytest.mark.parametrize("N,Nk,d,dv", [(30, 30, 12, 6), (77, 130, 64, 32), (200, 137, 96, 48),
+                                       (1, 9, 8, 8), (513, 1000, 128, 80)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_backward_padded_fast_path(fa, N, Nk, d, dv, dtype):
+    """16-bit shapes outside the MFMA kernels' (N, Nk % 8 == 0; d, dv in
+    {32, 64, 128}) run them on zero-padded workspace copies: against the oracle
+    and against the generic SIMT path on the same inputs (the reference test
+    shape (30, 12, 6) of test/test.jl:6-10 included)."""
+    tdt = torch.bfloat16 if dtype == "bfloat16" else torch.float16
+    rng = np.random.default_rng(N * 3 + Nk + d)
+    cast = lambda a: torch.tensor(a).to(tdt).double().numpy()
+    q, k = cast(rng.standard_normal((N, d, 2))), cast(rng.standard_normal((Nk, d, 2)))
+    v, do = cast(rng.standard_normal((Nk, dv, 2))), cast(rng.standard_normal((N, dv, 2)))
+    Q, K, V, dO = (fa.jl_tensor(a, tdt) for a in (q, k, v, do))
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    L = fa.lib()
+    padded = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
+    L.fa_debug_set_bwd_generic(1)
+    try:
+        gen = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
+    finally:
+        L.fa_debug_set_bwd_generic(0)
+    torch.cuda.synchronize()
+    dqr, dkr, dvr = O.dense_fa_backward(q, k, v, _np(Oo), do, _np(l), _np(m))
+    for a, g_, r_, nm in zip(padded, gen, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+        assert_grad_close(_np(a), r_, dtype, nm)
+        assert_grad_close(_np(a), _np(g_), dtype, nm + " vs generic")
