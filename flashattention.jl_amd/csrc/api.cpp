@@ -98,6 +98,30 @@ int fa_debug_set_win_composed(int v) {
     return old;
 }
 
+size_t fa_dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    if (!valid_dtype(dtype) || N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1) return 0;
+    return fa::dense_fwd_workspace(dtype, N, Nk, d, dv, batch);
+}
+
+int fa_dense_fwd_ws(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
+                    int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch, float scale,
+                    void* workspace, size_t workspace_bytes, void* hip_stream) {
+    static const char* fn = "fa_dense_fwd_ws";
+    if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
+    if (N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, d, dv, batch must be >= 1");
+    if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    const size_t need = fa::dense_fwd_workspace(dtype, N, Nk, d, dv, batch);
+    if (need > 0 && (!workspace || workspace_bytes < need))
+        return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_dense_fwd_workspace()");
+    fa::DenseArgs a{dtype, Q, K, V, O, l, m, N, Nk, d, dv, batch, resolve_scale(scale, d)};
+    a.workspace = workspace;
+    a.workspace_bytes = workspace_bytes;
+    const char* why = "";
+    const int rc = fa::launch_dense_fwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
 int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m,
                  int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch, float scale,
                  void* hip_stream) {

@@ -58,6 +58,7 @@ struct FwdParams {
     float* l;
     float* m;
     int N, Nk, d, dv;
+    int ldk;   // K / V row stride in elements (= Nk, or Nk rounded up to 8 in padded workspace copies)
     int nqb, total_wg;
     float scale, scale_log2;
     int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
@@ -489,8 +490,9 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     const int r = lane & 31, h = lane >> 5;
     const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
     const auto qrs = slab_rsrc((const T*)p.Q + (int64_t)b * N * d, (uint32_t)(N * d * (int)sizeof(T)));
-    const auto krs = slab_rsrc((const T*)p.K + (int64_t)b * Nk * d, (uint32_t)(Nk * d * (int)sizeof(T)));
-    const auto vrs = slab_rsrc((const T*)p.V + (int64_t)b * Nk * dv, (uint32_t)(Nk * dv * (int)sizeof(T)));
+    const int ldk = p.ldk;
+    const auto krs = slab_rsrc((const T*)p.K + (int64_t)b * ldk * d, (uint32_t)(ldk * d * (int)sizeof(T)));
+    const auto vrs = slab_rsrc((const T*)p.V + (int64_t)b * ldk * dv, (uint32_t)(ldk * dv * (int)sizeof(T)));
 
     int qiv[NQB];
     F8 qf[NQB][D / 16];
@@ -522,13 +524,13 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
 #pragma unroll
     for (int it = 0; it < KCH; ++it) {
         const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
-        kgo[it] = kact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
+        kgo[it] = kact ? (f * ldk + pc * 8) * 2 : 0x7FFFFFF0;
         kso[it] = kact ? f * KROW + (((pc >> 1) ^ kswz(f)) * 32) + (pc & 1) * 16 : 2 * STAGE;
     }
 #pragma unroll
     for (int it = 0; it < VCH; ++it) {
         const int ch = tid + NTH * it, f = ch / CPR, pc = ch % CPR;
-        vgo[it] = vact ? (f * Nk + pc * 8) * 2 : 0x7FFFFFF0;
+        vgo[it] = vact ? (f * ldk + pc * 8) * 2 : 0x7FFFFFF0;
         vso[it] = vact ? f * VROW + pc * 16 : 2 * STAGE - KBYTES;
     }
 
@@ -758,6 +760,33 @@ static hipError_t launch_f32(const FwdParams& p, int Dc, int DVc, dim3 grid, hip
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
+// Padded-key fast path: bf16/fp16 with Nk % 8 != 0 (or K / V not 16-B aligned)
+// copy K and V into zero-padded slabs of row stride Nk8 = roundup(Nk, 8) in the
+// caller's workspace; the fast kernels then address rows by ldk = Nk8 and mask
+// keys >= Nk as for any ragged last tile.  Without a workspace those shapes run
+// the generic kernel (fa_dense_fwd, no workspace argument).
+static bool fwd_pad_needed(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    const int64_t nk8 = (Nk + 7) / 8 * 8;
+    return dtype != FA_DTYPE_F32 && Nk % 8 != 0 && nk8 * d * 2 < INT32_MAX && nk8 * dv * 2 < INT32_MAX &&
+           nk8 * (d > dv ? d : dv) * batch < ((int64_t)1 << 40);
+}
+size_t dense_fwd_workspace(int dtype, int64_t, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    if (!fwd_pad_needed(dtype, Nk, d, dv, batch)) return 0;
+    const int64_t nk8 = (Nk + 7) / 8 * 8;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return al((size_t)(nk8 * d * batch) * 2) + al((size_t)(nk8 * dv * batch) * 2) + 256;
+}
+// dst (Np, C, B) <- src (N, C, B), zero rows n >= N
+template <class T>
+__global__ __launch_bounds__(256) void fwd_pad_keys(const T* __restrict__ src, T* __restrict__ dst, int N, int Np,
+                                                    int64_t total) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int n = (int)(e % Np);
+    const int64_t cb = e / Np;                  // c + C·b
+    dst[e] = n < N ? src[cb * N + n] : (T)0.0f;
+}
+
 int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     const int Dc = head_dim_class(a.d), DVc = head_dim_class(a.dv);
     if (!Dc || !DVc) {
@@ -782,11 +811,32 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
     const int epc = a.dtype == FA_DTYPE_F32 ? 4 : 8;
+    p.ldk = (int)a.Nk;
     p.fast = (a.Nk % epc == 0) && aligned16(a.K) && aligned16(a.V);
+    if (!p.fast && a.workspace && fwd_pad_needed(a.dtype, a.Nk, a.d, a.dv, a.batch) &&
+        a.N * a.d * 2 < (int64_t)INT32_MAX &&
+        a.workspace_bytes >= dense_fwd_workspace(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch)) {
+        const int64_t nk8 = (a.Nk + 7) / 8 * 8;
+        char* w = (char*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
+        char* kp = w;
+        char* vp = w + (((size_t)(nk8 * a.d * a.batch) * 2 + 255) & ~(size_t)255);
+        const int64_t tk = nk8 * a.d * a.batch, tv = nk8 * a.dv * a.batch;
+        if (a.dtype == FA_DTYPE_F16) {
+            hipLaunchKernelGGL(fwd_pad_keys<f16>, dim3((unsigned)((tk + 255) / 256)), dim3(256), 0, s, (const f16*)a.K, (f16*)kp, (int)a.Nk, (int)nk8, tk);
+            hipLaunchKernelGGL(fwd_pad_keys<f16>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, (const f16*)a.V, (f16*)vp, (int)a.Nk, (int)nk8, tv);
+        } else {
+            hipLaunchKernelGGL(fwd_pad_keys<bf16>, dim3((unsigned)((tk + 255) / 256)), dim3(256), 0, s, (const bf16*)a.K, (bf16*)kp, (int)a.Nk, (int)nk8, tk);
+            hipLaunchKernelGGL(fwd_pad_keys<bf16>, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, (const bf16*)a.V, (bf16*)vp, (int)a.Nk, (int)nk8, tv);
+        }
+        p.K = kp;
+        p.V = vp;
+        p.ldk = (int)nk8;
+        p.fast = 1;
+    }
     // buffer descriptors address a slab with 32-bit byte offsets
     const int64_t esz = a.dtype == FA_DTYPE_F32 ? 4 : 2;
-    if (a.N * a.d * esz >= (int64_t)INT32_MAX || a.Nk * a.d * esz >= (int64_t)INT32_MAX ||
-        a.Nk * a.dv * esz >= (int64_t)INT32_MAX)
+    if (a.N * a.d * esz >= (int64_t)INT32_MAX || (int64_t)p.ldk * a.d * esz >= (int64_t)INT32_MAX ||
+        (int64_t)p.ldk * a.dv * esz >= (int64_t)INT32_MAX)
         p.fast = 0;
     const dim3 grid((unsigned)total);
     hipError_t e;

@@ -15,6 +15,8 @@ struct DenseArgs {
     float *l, *m;
     int64_t N, Nk, d, dv, batch;
     float scale;               // already resolved (> 0)
+    void* workspace = nullptr; // optional: padded K / V copies for ragged Nk (fa_dense_fwd_workspace)
+    size_t workspace_bytes = 0;
 };
 
 struct DenseBwdArgs {
@@ -83,6 +85,7 @@ struct SoftmaxArgs {
 
 // Each returns a hipError_t-like code through *err and a fa_status.
 int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
+size_t dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why);
 size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);

@@ -116,6 +116,11 @@ def lib() -> ctypes.CDLL:
         getattr(L, wfn).restype = ctypes.c_int
         getattr(L, wfn).argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.POINTER(i64), i64, i64,
                                     i64, i64, i64, vp]
+    L.fa_dense_fwd_ws.restype = ctypes.c_int
+    L.fa_dense_fwd_ws.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp,
+                                  ctypes.c_size_t, vp]
+    L.fa_dense_fwd_workspace.restype = ctypes.c_size_t
+    L.fa_dense_fwd_workspace.argtypes = [ctypes.c_int, i64, i64, i64, i64, i64]
     L.fa_circulant_fwd.restype = ctypes.c_int
     L.fa_circulant_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp]
     L.fa_softmax_workspace.restype = ctypes.c_size_t
@@ -233,8 +238,15 @@ def dense_fa_(O: torch.Tensor, l: torch.Tensor, m: torch.Tensor,
     _require(l.dtype == torch.float32 and m.dtype == torch.float32, "l, m must be float32")
     code = _dtype_code(Q, K, V, O)
     _device_check(Q, K, V, O, l, m)
-    _check(lib().fa_dense_fwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
-                              N, Nk, d, dv, B, float(scale), _stream(Q)))
+    Lb = lib()
+    nws = Lb.fa_dense_fwd_workspace(code, N, Nk, d, dv, B)
+    if nws == 0:
+        _check(Lb.fa_dense_fwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
+                               N, Nk, d, dv, B, float(scale), _stream(Q)))
+    else:   # ragged Nk: padded K / V copies let the fast kernels run
+        ws = _workspace(Q.device, nws)
+        _check(Lb.fa_dense_fwd_ws(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
+                                  N, Nk, d, dv, B, float(scale), _ptr(ws), int(nws), _stream(Q)))
     return O, l, m
 
 

@@ -42,10 +42,20 @@ function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32
     size(K) == (Nk, d, B) || throw(DimensionMismatch("K"))
     size(V) == (Nk, dv, B) || throw(DimensionMismatch("V"))
     size(O) == (N, dv, B) || throw(DimensionMismatch("O"))
-    fa_check(ccall((:fa_dense_fwd, libfa_hip), Cint,
-                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
-                    Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
-                   fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, stream_ptr()))
+    nws = ccall((:fa_dense_fwd_workspace, libfa_hip), Csize_t,
+                (Cint, Int64, Int64, Int64, Int64, Int64), fa_dtype(T), N, Nk, d, dv, B)
+    if nws == 0
+        fa_check(ccall((:fa_dense_fwd, libfa_hip), Cint,
+                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                        Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
+                       fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, stream_ptr()))
+    else   # ragged Nk: zero-padded K / V copies in the workspace let the fast kernels run
+        ws = ROCArray{UInt8}(undef, Int(nws))
+        fa_check(ccall((:fa_dense_fwd_ws, libfa_hip), Cint,
+                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                        Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                       fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, ws, nws, stream_ptr()))
+    end
     return O, l, m
 end
 

@@ -65,6 +65,22 @@ int fa_dense_fwd(int dtype,
                  int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
                  float scale, void* hip_stream);
 
+/* fa_dense_fwd with a caller-owned workspace (same contract otherwise).  For
+ * bf16 / fp16 with Nk % 8 != 0 the workspace holds zero-padded K / V copies of
+ * row stride roundup(Nk, 8), so the ragged shape runs the fast MFMA kernels
+ * instead of the generic one (3.6-6x).  workspace may be NULL
+ * when fa_dense_fwd_workspace() returns 0. */
+int fa_dense_fwd_ws(int dtype,
+                    const void* Q, const void* K, const void* V,
+                    void* O, float* l, float* m,
+                    int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
+                    float scale, void* workspace, size_t workspace_bytes,
+                    void* hip_stream);
+
+/* Workspace bytes fa_dense_fwd_ws needs for these sizes (0 is a valid answer). */
+size_t fa_dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
+                              int64_t dv, int64_t batch);
+
 /* Workspace bytes fa_dense_bwd needs for these sizes (0 is a valid answer). */
 size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
                               int64_t dv, int64_t batch);

@@ -219,3 +219,31 @@ def test_long_single_slab(fa):
         assert_close(_np(y[r0:r0 + 128]), yr, "bfloat16", f"y[{r0}]")
         assert_lm_close(_np(l[r0:r0 + 128]), lr, "bfloat16", "l")
         assert_lm_close(_np(m[r0:r0 + 128]), mr, "bfloat16", "m")
+
+
+@pytest.mark.parametrize("N,Nk,d,dv", [(30, 30, 12, 6), (77, 130, 64, 32), (1000, 1001, 96, 48),
+                                       (257, 4095, 128, 128), (64, 9, 64, 64)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_forward_padded_keys_path(fa, N, Nk, d, dv, dtype):
+    """Ragged Nk through fa_dense_fwd_ws (zero-padded K / V copies, fast kernels)
+    against the oracle and against fa_dense_fwd without a workspace (generic kernel)."""
+    import ctypes
+    tdt = DT[dtype]
+    rng = np.random.default_rng(N + Nk + d)
+    cast = lambda a: torch.tensor(a).to(tdt).double().numpy()
+    q, k, v = cast(rng.standard_normal((N, d, 2))), cast(rng.standard_normal((Nk, d, 2))), cast(rng.standard_normal((Nk, dv, 2)))
+    Q, K, V = (fa.jl_tensor(a, tdt) for a in (q, k, v))
+    L = fa.lib()
+    code = fa._dtype_code(Q)
+    assert L.fa_dense_fwd_workspace(code, N, Nk, d, dv, 2) > 0
+    y1, l1, m1 = fa.dense_fa(Q, K, V)                     # workspace path
+    y2 = fa.jl_empty((N, dv, 2), tdt); l2 = fa.jl_empty((N, 1, 2)); m2 = fa.jl_empty((N, 1, 2))
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    assert L.fa_dense_fwd(code, P(Q), P(K), P(V), P(y2), P(l2), P(m2), N, Nk, d, dv, 2, 0.0,
+                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    yr, lr, mr = O.dense_fa3(q, k, v)
+    assert_close(_np(y1), yr, dtype, "y (padded keys)")
+    assert_lm_close(_np(l1), lr, dtype, "l")
+    assert_lm_close(_np(m1), mr, dtype, "m")
+    assert_close(_np(y1), _np(y2), dtype, "y padded vs generic")
