@@ -222,6 +222,194 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
 
 
 // --------------------------------------------------------------------------
+// 2./3. fp32 MFMA path (v_mfma_f32_32x32x2_f32: exact fp32 products, the same
+// arithmetic as an fmaf chain; d, dv <= 64, any N, Nk).  Each lane keeps its
+// own key's (dK/dV kernel) or query's (dQ kernel) K, V (resp. Q, dO) features in
+// registers as the B operand of the score products; the tile of the other side
+// sits in LDS ([feature][33] rows: conflict-free for both the column and the
+// row access).  The score accumulators are used directly as the B operand of
+// the gradient products: register x of lane (r, h) holds row acc_row(x, h), which
+// is exactly what a 32x32x2 B operand with k = h needs (cf. the fp32 forward).
+//   dK/dV: S = Q Kᵀ (queries on rows, keys on lanes), dVᵀ += dOᵀ P, dKᵀ += Qᵀ dS;
+//   dQ   : Sᵀ = K Qᵀ (keys on rows, queries on lanes), dQᵀ += Kᵀ dSᵀ.
+// Keys past Nk are zero rows: their own rows are not stored and their K = 0
+// adds nothing to dQ; queries past N carry nlse = −inf (P = 0) and dO = 0.
+// --------------------------------------------------------------------------
+constexpr int kF32T = 32;   // tile of the streamed side
+constexpr int kF32R = 33;   // LDS row (floats)
+
+template <int D, int DV>
+__global__ __launch_bounds__(256) void bwd_dkdv_f32(BwdParams p) {
+    __shared__ float sQ[D * kF32R], sdO[DV * kF32R], sL[kF32T], sD[kF32T];
+    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
+    const int nkb = (Nk + 127) / 128;
+    const int b = blockIdx.x / nkb, k0 = (blockIdx.x % nkb) * 128;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const float* Qb = (const float*)p.Q + (int64_t)b * N * d;
+    const float* dOb = (const float*)p.dO + (int64_t)b * N * dv;
+    const float* Kb = (const float*)p.K + (int64_t)b * Nk * d;
+    const float* Vb = (const float*)p.V + (int64_t)b * Nk * dv;
+    const int key = k0 + wave * 32 + r;
+    float kf[D / 2], vf[DV / 2];
+#pragma unroll
+    for (int t = 0; t < D / 2; ++t) kf[t] = (key < Nk && 2 * t + h < d) ? Kb[(int64_t)(2 * t + h) * Nk + key] : 0.0f;
+#pragma unroll
+    for (int t = 0; t < DV / 2; ++t) vf[t] = (key < Nk && 2 * t + h < dv) ? Vb[(int64_t)(2 * t + h) * Nk + key] : 0.0f;
+    f32x16 aK[D / 32], aV[DV / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) aK[i][x] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < DV / 32; ++i)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) aV[i][x] = 0.0f;
+    const float c = p.scale_log2;
+    const float* nD = p.nD + (int64_t)b * N;
+    const float* nL = p.nlse + (int64_t)b * N;
+    for (int q0 = 0; q0 < N; q0 += kF32T) {
+        __syncthreads();
+        for (int i = tid; i < D * kF32T; i += 256) {
+            const int q = i % kF32T, f = i / kF32T;
+            sQ[f * kF32R + q] = (q0 + q < N && f < d) ? Qb[(int64_t)f * N + q0 + q] : 0.0f;
+        }
+        for (int i = tid; i < DV * kF32T; i += 256) {
+            const int q = i % kF32T, f = i / kF32T;
+            sdO[f * kF32R + q] = (q0 + q < N && f < dv) ? dOb[(int64_t)f * N + q0 + q] : 0.0f;
+        }
+        if (tid < kF32T) {
+            sL[tid] = q0 + tid < N ? nL[q0 + tid] : kNegInf;
+            sD[tid] = q0 + tid < N ? nD[q0 + tid] : 0.0f;
+        }
+        __syncthreads();
+        f32x16 sa, pa;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) { sa[x] = 0.0f; pa[x] = 0.0f; }
+#pragma unroll
+        for (int t = 0; t < D / 2; ++t) sa = mfma32x32x2(sQ[(2 * t + h) * kF32R + r], kf[t], sa);
+#pragma unroll
+        for (int t = 0; t < DV / 2; ++t) pa = mfma32x32x2(sdO[(2 * t + h) * kF32R + r], vf[t], pa);
+        // lane (r, h): key r; register x: query acc_row(x, h)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int q = acc_row(x, h);
+            const float pr = exp2f((sa[x] + sL[q]) * c);
+            sa[x] = pr;                          // P
+            pa[x] = pr * (pa[x] + sD[q]);        // dS
+        }
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int q = acc_row(x, h);
+#pragma unroll
+            for (int i = 0; i < DV / 32; ++i) aV[i] = mfma32x32x2(sdO[(i * 32 + r) * kF32R + q], sa[x], aV[i]);
+#pragma unroll
+            for (int i = 0; i < D / 32; ++i) aK[i] = mfma32x32x2(sQ[(i * 32 + r) * kF32R + q], pa[x], aK[i]);
+        }
+    }
+    if (key < Nk) {
+        float* dKb = (float*)p.dK + (int64_t)b * Nk * d;
+        float* dVb = (float*)p.dV + (int64_t)b * Nk * dv;
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int f = i * 32 + acc_row(x, h);
+                if (f < d) dKb[(int64_t)f * Nk + key] = aK[i][x] * p.scale;
+            }
+#pragma unroll
+        for (int i = 0; i < DV / 32; ++i)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int f = i * 32 + acc_row(x, h);
+                if (f < dv) dVb[(int64_t)f * Nk + key] = aV[i][x];
+            }
+    }
+}
+
+template <int D, int DV>
+__global__ __launch_bounds__(256) void bwd_dq_f32(BwdParams p) {
+    __shared__ float sK[D * kF32R], sV[DV * kF32R];
+    const int N = p.N, Nk = p.Nk, d = p.d, dv = p.dv;
+    const int nqb = (N + 127) / 128;
+    const int b = blockIdx.x / nqb, q0 = (blockIdx.x % nqb) * 128;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const float* Qb = (const float*)p.Q + (int64_t)b * N * d;
+    const float* dOb = (const float*)p.dO + (int64_t)b * N * dv;
+    const float* Kb = (const float*)p.K + (int64_t)b * Nk * d;
+    const float* Vb = (const float*)p.V + (int64_t)b * Nk * dv;
+    const int qi = q0 + wave * 32 + r;
+    float qf[D / 2], df[DV / 2];
+#pragma unroll
+    for (int t = 0; t < D / 2; ++t) qf[t] = (qi < N && 2 * t + h < d) ? Qb[(int64_t)(2 * t + h) * N + qi] : 0.0f;
+#pragma unroll
+    for (int t = 0; t < DV / 2; ++t) df[t] = (qi < N && 2 * t + h < dv) ? dOb[(int64_t)(2 * t + h) * N + qi] : 0.0f;
+    const float nlq = qi < N ? p.nlse[(int64_t)b * N + qi] : kNegInf;
+    const float ndq = qi < N ? p.nD[(int64_t)b * N + qi] : 0.0f;
+    const float c = p.scale_log2;
+    f32x16 aQ[D / 32];
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) aQ[i][x] = 0.0f;
+    for (int k0 = 0; k0 < Nk; k0 += kF32T) {
+        __syncthreads();
+        for (int i = tid; i < D * kF32T; i += 256) {
+            const int k = i % kF32T, f = i / kF32T;
+            sK[f * kF32R + k] = (k0 + k < Nk && f < d) ? Kb[(int64_t)f * Nk + k0 + k] : 0.0f;
+        }
+        for (int i = tid; i < DV * kF32T; i += 256) {
+            const int k = i % kF32T, f = i / kF32T;
+            sV[f * kF32R + k] = (k0 + k < Nk && f < dv) ? Vb[(int64_t)f * Nk + k0 + k] : 0.0f;
+        }
+        __syncthreads();
+        f32x16 sa, pa;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) { sa[x] = 0.0f; pa[x] = 0.0f; }
+#pragma unroll
+        for (int t = 0; t < D / 2; ++t) sa = mfma32x32x2(sK[(2 * t + h) * kF32R + r], qf[t], sa);
+#pragma unroll
+        for (int t = 0; t < DV / 2; ++t) pa = mfma32x32x2(sV[(2 * t + h) * kF32R + r], df[t], pa);
+        // lane (r, h): query r; register x: key acc_row(x, h)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const float pr = exp2f((sa[x] + nlq) * c);
+            pa[x] = pr * (pa[x] + ndq);          // dSᵀ
+        }
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int k = acc_row(x, h);
+#pragma unroll
+            for (int i = 0; i < D / 32; ++i) aQ[i] = mfma32x32x2(sK[(i * 32 + r) * kF32R + k], pa[x], aQ[i]);
+        }
+    }
+    if (qi < N) {
+        float* dQb = (float*)p.dQ + (int64_t)b * N * d;
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int f = i * 32 + acc_row(x, h);
+                if (f < d) dQb[(int64_t)f * N + qi] = aQ[i][x] * p.scale;
+            }
+    }
+}
+
+template <int D, int DV>
+static hipError_t launch_f32_dd(const BwdParams& p, hipStream_t s) {
+    const int64_t nq = ((int64_t)p.N + 127) / 128 * p.batch, nk = ((int64_t)p.Nk + 127) / 128 * p.batch;
+    hipLaunchKernelGGL((bwd_dq_f32<D, DV>), dim3((unsigned)nq), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((bwd_dkdv_f32<D, DV>), dim3((unsigned)nk), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+static hipError_t launch_f32_mfma(const BwdParams& p, hipStream_t s) {
+    const int Dc = p.d <= 32 ? 32 : 64, DVc = p.dv <= 32 ? 32 : 64;
+    if (Dc == 32 && DVc == 32) return launch_f32_dd<32, 32>(p, s);
+    if (Dc == 32) return launch_f32_dd<32, 64>(p, s);
+    if (DVc == 32) return launch_f32_dd<64, 32>(p, s);
+    return launch_f32_dd<64, 64>(p, s);
+}
+
+// --------------------------------------------------------------------------
 // 2./3. MFMA fast path (bf16 / fp16; d, dv in {32, 64, 128}; N, Nk % 8 == 0;
 // 16-B aligned).  Token tiles of 64 are staged by LDS-DMA (buffer_load … lds)
 // into [rows][64 tokens] images with 128-B rows and a 16-B XOR swizzle
@@ -682,6 +870,8 @@ static hipError_t launch_typed(const BwdParams& p, hipStream_t s, bool fast) {
     if (e != hipSuccess) return e;
     if constexpr (!std::is_same<T, float>::value) {
         if (fast) return launch_fast<T>(p, s);
+    } else {
+        if (fast) return launch_f32_mfma(p, s);
     }
     return launch_generic<T>(p, s);
 }
@@ -766,7 +956,10 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     switch (a.dtype) {
         case FA_DTYPE_BF16: e = launch_typed<bf16>(p, s, fast); break;
         case FA_DTYPE_F16: e = launch_typed<f16>(p, s, fast); break;
-        case FA_DTYPE_F32: e = launch_typed<float>(p, s, false); break;
+        case FA_DTYPE_F32:   // fp32 MFMA kernels for d, dv <= 64 (exact fp32 products)
+            e = launch_typed<float>(p, s, !g_bwd_force_generic && a.d <= 64 && a.dv <= 64 &&
+                                              a.N * a.batch < INT32_MAX / 2 && a.Nk * a.batch < INT32_MAX / 2);
+            break;
         default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
     }
     if (e != hipSuccess) {

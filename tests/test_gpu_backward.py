@@ -181,3 +181,28 @@ def test_backward_padded_fast_path(fa, N, Nk, d, dv, dtype):
     for a, g_, r_, nm in zip(padded, gen, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
         assert_grad_close(_np(a), r_, dtype, nm)
         assert_grad_close(_np(a), _np(g_), dtype, nm + " vs generic")
+
+
+@pytest.mark.parametrize("N,Nk,d,dv", [(30, 30, 12, 6), (200, 137, 64, 48), (256, 256, 64, 64),
+                                       (1, 70, 32, 64), (513, 300, 40, 24)])
+def test_backward_f32_mfma_path(fa, N, Nk, d, dv):
+    """fp32 (d, dv <= 64) runs on v_mfma_f32_32x32x2_f32 (exact fp32 products):
+    against the float64 oracle at the fp32 tolerance and against the generic
+    SIMT path on the same inputs."""
+    rng = np.random.default_rng(N * 5 + Nk + d)
+    q, k = rng.standard_normal((N, d, 2)), rng.standard_normal((Nk, d, 2))
+    v, do = rng.standard_normal((Nk, dv, 2)), rng.standard_normal((N, dv, 2))
+    Q, K, V, dO = (fa.jl_tensor(a, torch.float32) for a in (q, k, v, do))
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    L = fa.lib()
+    mf = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
+    L.fa_debug_set_bwd_generic(1)
+    try:
+        gen = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
+    finally:
+        L.fa_debug_set_bwd_generic(0)
+    torch.cuda.synchronize()
+    dqr, dkr, dvr = O.dense_fa_backward(q, k, v, _np(Oo), do, _np(l), _np(m))
+    for a, g_, r_, nm in zip(mf, gen, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+        assert_grad_close(_np(a), r_, "float32", nm)
+        assert_grad_close(_np(a), _np(g_), "float32", nm + " vs generic")

@@ -25,3 +25,13 @@ q, k, v, dy = (_randn_jl(fa_hip, (128, 128, 64, 1), torch.bfloat16, g) for _ in 
 y, lw, mw = fa_hip.windowed_fa(q, k, v, 7, stride=4)
 t = time_graph(lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7, stride=4), 10)
 print(f"windowed backward 128x128x64 ws 7 stride 4 (overlapping, composed): {t*1e6:.1f} us", flush=True)
+for (N, d, B) in [(4096, 64, 64), (512, 64, 4)]:
+    Q, K, V, dO = (fa_hip.jl_tensor(torch.randn((N, d, B), device="cuda"), torch.float32) for _ in range(4))
+    O, l, m = fa_hip.dense_fa(Q, K, V)
+    res = []
+    for gen in (0, 1):
+        L.fa_debug_set_bwd_generic(gen)
+        res.append(time_graph(lambda: fa_hip.dense_fa_backward(Q, K, V, O, dO, l, m), 3))
+    L.fa_debug_set_bwd_generic(0)
+    fl = 10.0 * B * N * N * d
+    print(f"fp32 N={N} d={d} B={B}: mfma {res[0]*1e6:9.1f} us ({fl/res[0]/1e12:6.1f} TF)  generic {res[1]*1e6:9.1f} us  x{res[1]/res[0]:.1f}", flush=True)
