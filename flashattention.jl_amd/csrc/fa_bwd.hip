@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
 
 // --------------------------------------------------------------------------
 // 2./3. fp32 MFMA path (v_mfma_f32_32x32x2_f32: exact fp32 products, the same
-// arithmetic as an fmaf chain; d, dv <= 64, any N, Nk).  Each lane keeps its
+// arithmetic as an fmaf chain; d, dv <= 128 (classes 32 / 64 / 128), any N, Nk).  Each lane keeps its
 // own key's (dK/dV kernel) or query's (dQ kernel) K, V (resp. Q, dO) features in
 // registers as the B operand of the score products; the tile of the other side
 // sits in LDS ([feature][33] rows: conflict-free for both the column and the
@@ -402,6 +402,7 @@ static hipError_t launch_f32_dd(const BwdParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 static hipError_t launch_f32_mfma(const BwdParams& p, hipStream_t s) {
+    if (p.d > 64 || p.dv > 64) return launch_f32_dd<128, 128>(p, s);
     const int Dc = p.d <= 32 ? 32 : 64, DVc = p.dv <= 32 ? 32 : 64;
     if (Dc == 32 && DVc == 32) return launch_f32_dd<32, 32>(p, s);
     if (Dc == 32) return launch_f32_dd<32, 64>(p, s);
@@ -956,8 +957,8 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     switch (a.dtype) {
         case FA_DTYPE_BF16: e = launch_typed<bf16>(p, s, fast); break;
         case FA_DTYPE_F16: e = launch_typed<f16>(p, s, fast); break;
-        case FA_DTYPE_F32:   // fp32 MFMA kernels for d, dv <= 64 (exact fp32 products)
-            e = launch_typed<float>(p, s, !g_bwd_force_generic && a.d <= 64 && a.dv <= 64 &&
+        case FA_DTYPE_F32:   // fp32 MFMA kernels (exact fp32 products)
+            e = launch_typed<float>(p, s, !g_bwd_force_generic &&
                                               a.N * a.batch < INT32_MAX / 2 && a.Nk * a.batch < INT32_MAX / 2);
             break;
         default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;

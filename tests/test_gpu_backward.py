@@ -184,9 +184,10 @@ def test_backward_padded_fast_path(fa, N, Nk, d, dv, dtype):
 
 
 @pytest.mark.parametrize("N,Nk,d,dv", [(30, 30, 12, 6), (200, 137, 64, 48), (256, 256, 64, 64),
-                                       (1, 70, 32, 64), (513, 300, 40, 24)])
+                                       (1, 70, 32, 64), (513, 300, 40, 24), (130, 200, 128, 128),
+                                       (64, 64, 96, 16)])
 def test_backward_f32_mfma_path(fa, N, Nk, d, dv):
-    """fp32 (d, dv <= 64) runs on v_mfma_f32_32x32x2_f32 (exact fp32 products):
+    """fp32 (d, dv <= 128) runs on v_mfma_f32_32x32x2_f32 (exact fp32 products):
     against the float64 oracle at the fp32 tolerance and against the generic
     SIMT path on the same inputs."""
     rng = np.random.default_rng(N * 5 + Nk + d)

@@ -25,7 +25,7 @@ q, k, v, dy = (_randn_jl(fa_hip, (128, 128, 64, 1), torch.bfloat16, g) for _ in 
 y, lw, mw = fa_hip.windowed_fa(q, k, v, 7, stride=4)
 t = time_graph(lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7, stride=4), 10)
 print(f"windowed backward 128x128x64 ws 7 stride 4 (overlapping, composed): {t*1e6:.1f} us", flush=True)
-for (N, d, B) in [(4096, 64, 64), (512, 64, 4)]:
+for (N, d, B) in [(4096, 64, 64), (512, 64, 4), (2048, 128, 16)]:
     Q, K, V, dO = (fa_hip.jl_tensor(torch.randn((N, d, B), device="cuda"), torch.float32) for _ in range(4))
     O, l, m = fa_hip.dense_fa(Q, K, V)
     res = []
