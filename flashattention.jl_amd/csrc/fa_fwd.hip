@@ -60,6 +60,11 @@ struct FwdParams {
     int N, Nk, d, dv;
     int ldk;   // K / V row stride in elements (= Nk, or Nk rounded up to 8 in padded workspace copies)
     int nqb, total_wg;
+    // split-KV (small grids): nsplit key ranges of tps tiles each; partial results
+    // (fp32, unnormalised, relative to the split's max) go to opart / lpart / mpart,
+    // indexed by (split * batch + b)
+    int nsplit, tps, batch;
+    float *opart, *lpart, *mpart;
     float scale, scale_log2;
     int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
 };
@@ -483,7 +488,9 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     // f+1 are 32 banks apart already; 256-B rows need a 2-bit XOR).
     auto kswz = [](int f) { return BN == 64 ? (((f >> 1) & 1) << 1) : ((f & 3) << 1); };
 
-    const int lid = xcd_remap(blockIdx.x, p.total_wg);
+    int lid = xcd_remap(blockIdx.x, p.total_wg);
+    const int split = p.nsplit > 1 ? lid % p.nsplit : 0;
+    if (p.nsplit > 1) lid /= p.nsplit;
     const int b = lid / p.nqb;
     const int qb = lid - b * p.nqb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -644,20 +651,47 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
 
     char* const buf0 = smem;
     char* const buf1 = smem + STAGE;
-    gload(0);
-    lstore(buf0, 0);
+    // key tiles [jt0, jt1) of this workgroup (all tiles unless split-KV)
+    const int jt0 = split * p.tps, jt1 = p.nsplit > 1 ? min(NT, jt0 + p.tps) : NT;
+    gload(jt0);
+    lstore(buf0, jt0);
     __syncthreads();
-    for (int j = 0; j < NT; j += 2) {
-        gload(min(j + 1, NT - 1));
+    for (int j = jt0; j < jt1; j += 2) {
+        gload(min(j + 1, jt1 - 1));
         compute(buf0, buf0 + KBYTES, j);
-        lstore(buf1, min(j + 1, NT - 1));
+        lstore(buf1, min(j + 1, jt1 - 1));
         __syncthreads();
-        if (j + 1 < NT) {
-            gload(min(j + 2, NT - 1));
+        if (j + 1 < jt1) {
+            gload(min(j + 2, jt1 - 1));
             compute(buf1, buf1 + KBYTES, j + 1);
-            lstore(buf0, min(j + 2, NT - 1));
+            lstore(buf0, min(j + 2, jt1 - 1));
             __syncthreads();
         }
+    }
+
+    if (p.nsplit > 1) {   // partials: O, l relative to exp2(c (s - m_true)), m_true in raw units
+        const int64_t sb = (int64_t)split * p.batch + b;
+#pragma unroll
+        for (int u = 0; u < NQB; ++u) {
+            const int qi = qiv[u];
+            const float sc = exp2_fast((m_used[u] - m_true[u]) * c);
+            const float lt = swap_halves_sum(l_run[u]) * sc;
+            if (qi < N) {
+                float* Op = p.opart + sb * N * dv;
+#pragma unroll
+                for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) {
+                        const int cc = cb * 32 + acc_row(x, h);
+                        if (cc < dv) Op[(int64_t)cc * N + qi] = oacc[u][cb][x] * sc;
+                    }
+                if (h == 0) {
+                    p.mpart[sb * N + qi] = m_true[u];
+                    p.lpart[sb * N + qi] = lt;
+                }
+            }
+        }
+        return;
     }
 
 #pragma unroll
@@ -691,6 +725,60 @@ __global__ __launch_bounds__(256, 2) void dense_fwd_w4q2(FwdParams p) { dense_fw
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
 
+// Split-KV combine: O = Σ_s o_s·2^(c(m_s − m)) / Σ_s l_s·2^(c(m_s − m)), m = max_s m_s
+// (fixed split order: deterministic).  One thread per output element.
+template <class T>
+__global__ __launch_bounds__(256) void fwd_split_combine(FwdParams p, int64_t total) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int N = p.N, dv = p.dv, B = p.batch;
+    const int n = (int)(e % N);
+    const int64_t rest = e / N;
+    const int cc = (int)(rest % dv);
+    const int b = (int)(rest / dv);
+    const float c = p.scale_log2;
+    float mx = kNegInf;
+    for (int sp = 0; sp < p.nsplit; ++sp) mx = vmax(mx, p.mpart[((int64_t)sp * B + b) * N + n]);
+    float L = 0.0f, acc = 0.0f;
+    for (int sp = 0; sp < p.nsplit; ++sp) {
+        const int64_t sb = (int64_t)sp * B + b;
+        const float w = exp2_fast((p.mpart[sb * N + n] - mx) * c);
+        L = fmaf(p.lpart[sb * N + n], w, L);
+        acc = fmaf(p.opart[(sb * dv + cc) * N + n], w, acc);
+    }
+    ((T*)p.O)[((int64_t)b * dv + cc) * N + n] = (T)(acc / L);
+    if (cc == 0) {
+        p.m[(int64_t)b * N + n] = mx * p.scale;
+        p.l[(int64_t)b * N + n] = L;
+    }
+}
+
+// Split-KV plan for the fast kernels: grids of fewer workgroups than CUs split the
+// key range so that ~512 workgroups run (each at least 2 tiles of 64 keys).
+struct SplitPlan {
+    int nsplit = 1, tps = 0;
+    size_t bytes = 0;
+};
+static SplitPlan split_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    SplitPlan sp;
+    const int Dc = head_dim_class(d), DVc = head_dim_class(dv);
+    if (dtype == FA_DTYPE_F32 || !Dc || !DVc) return sp;
+    const int64_t rows = (Dc <= 64 && DVc <= 64) ? 512 : 256;
+    const int64_t wgs = (N + rows - 1) / rows * batch;
+    const int64_t NT = (Nk + kBN - 1) / kBN;
+    if (wgs >= 256 || NT < 4) return sp;
+    int64_t ns = std::min<int64_t>((512 + wgs - 1) / wgs, NT / 2);
+    if (ns < 2) return sp;
+    const int64_t tps = (NT + ns - 1) / ns;
+    ns = (NT + tps - 1) / tps;
+    if (ns < 2 || ns * wgs > INT32_MAX) return sp;
+    sp.nsplit = (int)ns;
+    sp.tps = (int)tps;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    sp.bytes = al((size_t)(ns * batch * N * dv) * 4) + 2 * al((size_t)(ns * batch * N) * 4) + 256;
+    return sp;
+}
+
 // --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
@@ -705,7 +793,7 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         const int nqb = v >= 6 ? 2 : 1;
         FwdParams q = p;
         q.nqb = (q.N + 32 * nw * nqb - 1) / (32 * nw * nqb);
-        q.total_wg = q.nqb * (int)(p.total_wg / p.nqb);
+        q.total_wg = q.nqb * (int)(p.total_wg / p.nqb) * (q.nsplit > 1 ? q.nsplit : 1);
         const dim3 g2((unsigned)q.total_wg);
         const dim3 blk(64 * nw);
 #define FA_LAUNCH_T(KER)                                                                \
@@ -720,6 +808,10 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
         else { FA_LAUNCH_T(dense_fwd_w8q2) }
 #undef FA_LAUNCH_T
+        if (q.nsplit > 1) {
+            const int64_t total = (int64_t)q.N * q.dv * q.batch;
+            hipLaunchKernelGGL(fwd_split_combine<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, q, total);
+        }
         return hipGetLastError();
     }
     switch (DVc) {
@@ -770,11 +862,14 @@ static bool fwd_pad_needed(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t
     return dtype != FA_DTYPE_F32 && Nk % 8 != 0 && nk8 * d * 2 < INT32_MAX && nk8 * dv * 2 < INT32_MAX &&
            nk8 * (d > dv ? d : dv) * batch < ((int64_t)1 << 40);
 }
-size_t dense_fwd_workspace(int dtype, int64_t, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+static size_t fwd_pad_bytes(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     if (!fwd_pad_needed(dtype, Nk, d, dv, batch)) return 0;
     const int64_t nk8 = (Nk + 7) / 8 * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     return al((size_t)(nk8 * d * batch) * 2) + al((size_t)(nk8 * dv * batch) * 2) + 256;
+}
+size_t dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    return fwd_pad_bytes(dtype, Nk, d, dv, batch) + split_plan(dtype, N, Nk, d, dv, batch).bytes;
 }
 // dst (Np, C, B) <- src (N, C, B), zero rows n >= N
 template <class T>
@@ -810,12 +905,15 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     p.total_wg = (int)total;
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
+    p.batch = (int)a.batch;
+    p.nsplit = 1; p.tps = 0; p.opart = p.lpart = p.mpart = nullptr;
     const int epc = a.dtype == FA_DTYPE_F32 ? 4 : 8;
     p.ldk = (int)a.Nk;
+    const size_t pad_bytes = fwd_pad_bytes(a.dtype, a.Nk, a.d, a.dv, a.batch);
     p.fast = (a.Nk % epc == 0) && aligned16(a.K) && aligned16(a.V);
     if (!p.fast && a.workspace && fwd_pad_needed(a.dtype, a.Nk, a.d, a.dv, a.batch) &&
         a.N * a.d * 2 < (int64_t)INT32_MAX &&
-        a.workspace_bytes >= dense_fwd_workspace(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch)) {
+        a.workspace_bytes >= pad_bytes) {
         const int64_t nk8 = (a.Nk + 7) / 8 * 8;
         char* w = (char*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
         char* kp = w;
@@ -838,6 +936,22 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     if (a.N * a.d * esz >= (int64_t)INT32_MAX || (int64_t)p.ldk * a.d * esz >= (int64_t)INT32_MAX ||
         (int64_t)p.ldk * a.dv * esz >= (int64_t)INT32_MAX)
         p.fast = 0;
+    // split-KV for small grids (fast kernels, default geometry, workspace given)
+    if (p.fast && g_fwd_variant == 0 && a.workspace) {
+        const SplitPlan sp = split_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
+        if (sp.nsplit > 1 && a.workspace_bytes >= pad_bytes + sp.bytes) {
+            auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+            char* w = (char*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255) + (pad_bytes ? pad_bytes - 256 : 0);
+            w = (char*)(((uintptr_t)w + 255) & ~(uintptr_t)255);
+            p.opart = (float*)w;
+            w += al((size_t)(sp.nsplit * a.batch * a.N * a.dv) * 4);
+            p.lpart = (float*)w;
+            w += al((size_t)(sp.nsplit * a.batch * a.N) * 4);
+            p.mpart = (float*)w;
+            p.nsplit = sp.nsplit;
+            p.tps = sp.tps;
+        }
+    }
     const dim3 grid((unsigned)total);
     hipError_t e;
     switch (a.dtype) {

@@ -247,3 +247,32 @@ def test_forward_padded_keys_path(fa, N, Nk, d, dv, dtype):
     assert_lm_close(_np(l1), lr, dtype, "l")
     assert_lm_close(_np(m1), mr, dtype, "m")
     assert_close(_np(y1), _np(y2), dtype, "y padded vs generic")
+
+
+@pytest.mark.parametrize("N,Nk,d,dv,B", [(512, 512, 64, 64, 1), (4096, 4096, 64, 64, 1), (128, 32768, 128, 128, 2),
+                                         (1000, 3001, 96, 48, 1), (33, 4096, 32, 64, 3), (16384, 2048, 64, 64, 1)])
+def test_forward_split_kv(fa, N, Nk, d, dv, B):
+    """Small grids split the key range over workgroups (fp32 partials + an
+    ordered combine): against the oracle on every slab, and against the unsplit
+    kernel (fa_dense_fwd without a workspace) on the same inputs."""
+    import ctypes
+    rng = np.random.default_rng(N + Nk + d + B)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    q, k, v = bf(rng.standard_normal((N, d, B))), bf(rng.standard_normal((Nk, d, B))), bf(rng.standard_normal((Nk, dv, B)))
+    Q, K, V = (fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v))
+    L = fa.lib()
+    assert L.fa_dense_fwd_workspace(fa._dtype_code(Q), N, Nk, d, dv, B) > 0, "expected a split plan"
+    y1, l1, m1 = fa.dense_fa(Q, K, V)
+    y2 = fa.jl_empty((N, dv, B), torch.bfloat16); l2 = fa.jl_empty((N, 1, B)); m2 = fa.jl_empty((N, 1, B))
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    assert L.fa_dense_fwd(fa._dtype_code(Q), P(Q), P(K), P(V), P(y2), P(l2), P(m2), N, Nk, d, dv, B, 0.0,
+                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    if N * Nk <= 4096 * 4096:
+        yr, lr, mr = O.dense_fa3(q, k, v)
+        assert_close(_np(y1), yr, "bfloat16", "y split")
+        assert_lm_close(_np(l1), lr, "bfloat16", "l split")
+        assert_lm_close(_np(m1), mr, "bfloat16", "m split")
+    assert_close(_np(y1), _np(y2), "bfloat16", "y split vs unsplit")
+    assert np.array_equal(_np(m1), _np(m2)), "m is the exact row max either way"
+    assert_lm_close(_np(l1), _np(l2), "bfloat16", "l split vs unsplit")
