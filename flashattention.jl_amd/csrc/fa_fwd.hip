@@ -465,7 +465,7 @@ __global__ __launch_bounds__(kThreads) void dense_fwd_generic_f32(FwdParams p) {
 // barrier per tile, lazy rescale, branch-free buffer loads).  The partial-tile
 // V zeroing runs only on the last tile.
 // --------------------------------------------------------------------------
-template <class T, int D, int DV, int NW, int BN, int NQB>
+template <class T, int D, int DV, int NW, int BN, int NQB, bool SPLIT = false>
 __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
@@ -489,8 +489,8 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     auto kswz = [](int f) { return BN == 64 ? (((f >> 1) & 1) << 1) : ((f & 3) << 1); };
 
     int lid = xcd_remap(blockIdx.x, p.total_wg);
-    const int split = p.nsplit > 1 ? lid % p.nsplit : 0;
-    if (p.nsplit > 1) lid /= p.nsplit;
+    const int split = SPLIT ? lid % p.nsplit : 0;
+    if (SPLIT) lid /= p.nsplit;
     const int b = lid / p.nqb;
     const int qb = lid - b * p.nqb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -652,7 +652,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     char* const buf0 = smem;
     char* const buf1 = smem + STAGE;
     // key tiles [jt0, jt1) of this workgroup (all tiles unless split-KV)
-    const int jt0 = split * p.tps, jt1 = p.nsplit > 1 ? min(NT, jt0 + p.tps) : NT;
+    const int jt0 = SPLIT ? split * p.tps : 0, jt1 = SPLIT ? min(NT, jt0 + p.tps) : NT;
     gload(jt0);
     lstore(buf0, jt0);
     __syncthreads();
@@ -669,7 +669,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         }
     }
 
-    if (p.nsplit > 1) {   // partials: O, l relative to exp2(c (s - m_true)), m_true in raw units
+    if constexpr (SPLIT) {   // partials: O, l relative to exp2(c (s - m_true)), m_true in raw units
         const int64_t sb = (int64_t)split * p.batch + b;
 #pragma unroll
         for (int u = 0; u < NQB; ++u) {
@@ -724,6 +724,11 @@ template <class T, int D, int DV>
 __global__ __launch_bounds__(256, 2) void dense_fwd_w4q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 4, 64, 2>(p); }
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
+// split-KV instantiations of the two default geometries (small grids)
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void dense_fwd_w8q2_split(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2, true>(p); }
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void dense_fwd_w8b64_split(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 1, true>(p); }
 
 // Split-KV combine: O = Σ_s o_s·2^(c(m_s − m)) / Σ_s l_s·2^(c(m_s − m)), m = max_s m_s
 // (fixed split order: deterministic).  One thread per output element.
@@ -803,7 +808,9 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
             case 128: hipLaunchKernelGGL((KER<T, D, 128>), g2, blk, 0, s, q); break;    \
             default: return hipErrorInvalidValue;                                       \
         }
-        if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
+        if (q.nsplit > 1 && v == 5) { FA_LAUNCH_T(dense_fwd_w8b64_split) }
+        else if (q.nsplit > 1) { FA_LAUNCH_T(dense_fwd_w8q2_split) }
+        else if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
         else if (v == 5) { FA_LAUNCH_T(dense_fwd_w8b64) }
         else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
         else { FA_LAUNCH_T(dense_fwd_w8q2) }

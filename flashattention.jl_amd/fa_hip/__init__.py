@@ -112,15 +112,18 @@ def lib() -> ctypes.CDLL:
     L.fa_windowed_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                   ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, i64,
                                   f32, vp, ctypes.c_size_t, vp]
+    # (hasattr: tools/ab_lib.py also loads older builds for A/B timing)
     for wfn in ("fa_window", "fa_unwindow"):
-        getattr(L, wfn).restype = ctypes.c_int
-        getattr(L, wfn).argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.POINTER(i64), i64, i64,
-                                    i64, i64, i64, vp]
-    L.fa_dense_fwd_ws.restype = ctypes.c_int
-    L.fa_dense_fwd_ws.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp,
-                                  ctypes.c_size_t, vp]
-    L.fa_dense_fwd_workspace.restype = ctypes.c_size_t
-    L.fa_dense_fwd_workspace.argtypes = [ctypes.c_int, i64, i64, i64, i64, i64]
+        if hasattr(L, wfn):
+            getattr(L, wfn).restype = ctypes.c_int
+            getattr(L, wfn).argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.POINTER(i64), i64, i64,
+                                        i64, i64, i64, vp]
+    if hasattr(L, "fa_dense_fwd_ws"):
+        L.fa_dense_fwd_ws.restype = ctypes.c_int
+        L.fa_dense_fwd_ws.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp,
+                                      ctypes.c_size_t, vp]
+        L.fa_dense_fwd_workspace.restype = ctypes.c_size_t
+        L.fa_dense_fwd_workspace.argtypes = [ctypes.c_int, i64, i64, i64, i64, i64]
     L.fa_circulant_fwd.restype = ctypes.c_int
     L.fa_circulant_fwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, vp]
     L.fa_softmax_workspace.restype = ctypes.c_size_t
@@ -239,7 +242,7 @@ def dense_fa_(O: torch.Tensor, l: torch.Tensor, m: torch.Tensor,
     code = _dtype_code(Q, K, V, O)
     _device_check(Q, K, V, O, l, m)
     Lb = lib()
-    nws = Lb.fa_dense_fwd_workspace(code, N, Nk, d, dv, B)
+    nws = Lb.fa_dense_fwd_workspace(code, N, Nk, d, dv, B) if hasattr(Lb, "fa_dense_fwd_ws") else 0
     if nws == 0:
         _check(Lb.fa_dense_fwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
                                N, Nk, d, dv, B, float(scale), _stream(Q)))
