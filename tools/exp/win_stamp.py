@@ -31,9 +31,10 @@ for rep in range(3):
     rc = L.stamp_run(P(q), P(k), P(v), P(y), P(l), P(m), Bimg, out.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0, rc
     s = out.reshape(-1, 8).astype(np.int64)
+    s[:, 1] = s[:, 0]          # the row-shift kernel has no stamp 1 (no separate zero-fill phase)
     ph = np.diff(s[:, :6], axis=1)
     rt0, rt1 = s[:, 6], s[:, 7]
-    names = ["issue loads + zero LDS + sync", "scatter + sync", "QK", "softmax", "PV + stores"]
+    names = ["-", "loads + stage + sync", "QK", "softmax", "PV + stores"]
     print(f"rep {rep}: per-WG phase cycles (median / p90): " +
           ", ".join(f"{n}: {np.median(ph[:, i]):.0f}/{np.percentile(ph[:, i], 90):.0f}" for i, n in enumerate(names)))
     print(f"   WG total cycles median {np.median(s[:, 5] - s[:, 0]):.0f}; realtime (100 MHz ticks): WG span median "
