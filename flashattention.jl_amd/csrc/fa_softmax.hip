@@ -233,40 +233,82 @@ __global__ __launch_bounds__(kSmThreads) void sm_cols_reg_v(const T* S, T* P, in
 // merge their (max, Σexp) partials through LDS, then each writes its columns.
 template <class T>
 __global__ __launch_bounds__(kSmThreads) void sm_rows_v(const T* S, T* P, int64_t M, int N) {
-    constexpr int VEC = SmVec<T>::n, NWV = kSmThreads / 64;
+    // Both passes stream the row block U columns at a time (U independent 16-B
+    // loads in flight per lane).  Pass 1 merges each U-column chunk into the
+    // running (m, l) with ONE rescale: chunk max (IEEE maximum: NaN propagates),
+    // then l = l·e^(m−m') + Σ e^(f−m'); a chunk whose max is −inf changes nothing
+    // (as ml_merge's guard), so leading −inf columns cannot poison l.
+    constexpr int VEC = SmVec<T>::n, NWV = kSmThreads / 64, U = 8;
     __shared__ float pm[NWV][64 * VEC], pl[NWV][64 * VEC];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t i0 = ((int64_t)blockIdx.x * 64 + lane) * VEC;
     const bool act = i0 < M;
     const int64_t base = (int64_t)blockIdx.y * M * N + i0;
-    float m[VEC], l[VEC], f[VEC];
+    float m[VEC], l[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) { m[k] = kNegInf; l[k] = 0.f; }
     if (act) {
-        for (int j = wave; j < N; j += NWV) {
-            unpack16<T>(*(const u32x4*)(S + base + (int64_t)j * M), f);
+        for (int j0 = wave; j0 < N; j0 += NWV * U) {
+            u32x4 raw[U];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) ml_merge(m[k], l[k], f[k], 1.0f);
+            for (int u = 0; u < U; ++u) {
+                const int j = j0 + NWV * u;
+                raw[u] = j < N ? *(const u32x4*)(S + base + (int64_t)j * M) : u32x4{0u, 0u, 0u, 0u};
+            }
+            float f[U][VEC];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                unpack16<T>(raw[u], f[u]);
+                if (j0 + NWV * u >= N)
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) f[u][k] = kNegInf;
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                float cm = f[0][k];
+#pragma unroll
+                for (int u = 1; u < U; ++u) cm = vmax(cm, f[u][k]);
+                const float mn = vmax(m[k], cm);
+                float add = 0.0f;
+#pragma unroll
+                for (int u = 0; u < U; ++u) add += exp2_fast((f[u][k] - mn) * kLog2e);
+                const bool skip = mn == kNegInf;
+                l[k] = skip ? l[k] : fmaf(l[k], exp2_fast((m[k] - mn) * kLog2e), add);
+                m[k] = skip ? m[k] : mn;
+            }
         }
     }
 #pragma unroll
     for (int k = 0; k < VEC; ++k) { pm[wave][lane * VEC + k] = m[k]; pl[wave][lane * VEC + k] = l[k]; }
     __syncthreads();
-    float inv[VEC];
+    float mrow[VEC], inv[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
         float mm = pm[0][lane * VEC + k], ll = pl[0][lane * VEC + k];
 #pragma unroll
         for (int w = 1; w < NWV; ++w) ml_merge(mm, ll, pm[w][lane * VEC + k], pl[w][lane * VEC + k]);
-        m[k] = mm;
+        mrow[k] = mm;
         inv[k] = 1.0f / ll;
     }
     if (!act) return;
-    for (int j = wave; j < N; j += NWV) {
-        unpack16<T>(*(const u32x4*)(S + base + (int64_t)j * M), f);
+    for (int j0 = wave; j0 < N; j0 += NWV * U) {
+        u32x4 raw[U];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) f[k] = __expf(f[k] - m[k]) * inv[k];
-        *(u32x4*)(P + base + (int64_t)j * M) = pack16<T>(f);
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + NWV * u;
+            if (j < N) raw[u] = *(const u32x4*)(S + base + (int64_t)j * M);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + NWV * u;
+            if (j < N) {
+                float f[VEC];
+                unpack16<T>(raw[u], f);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) f[k] = exp2_fast((f[k] - mrow[k]) * kLog2e) * inv[k];
+                *(u32x4*)(P + base + (int64_t)j * M) = pack16<T>(f);
+            }
+        }
     }
 }
 
