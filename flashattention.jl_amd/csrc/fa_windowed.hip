@@ -1131,6 +1131,152 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     }
 }
 
+// --------------------------------------------------------------------------
+// fp32 fused windowed forward (2-D, stride >= ws, ws <= 8, d, dv <= 64, W >= 8):
+// one window per workgroup on the exact-f32 MFMA v_mfma_f32_32x32x2_f32 (the
+// arithmetic of an fmaf chain, like the fp32 dense path).  Staging: each
+// (feature, window row) item is two 16-B loads of the 8 pixels starting at
+// a = clamp(xs, 0, W - 8) (fp32 pixels are dword aligned, so the window-uniform
+// shift xs - a is a dword select), masked (slot < ws, pixel in the image) and
+// written to [feature][65-float] LDS rows (conflict-free for both the column
+// reads of the score product and the row reads of the PV product).  Wave
+// (qb, vc): Sᵀ = K·Qᵀ for query block qb, exact softmax per query, then
+// Oᵀ = Vᵀ·Pᵀ for its 32-feature chunk with the score accumulators as the B
+// operand (register x of lane (r, h) holds key acc_row(x, h): k = h).
+// --------------------------------------------------------------------------
+template <int D, int DV>
+__global__ __launch_bounds__(256) void win_rows_f32(const float* __restrict__ q, const float* __restrict__ k,
+                                                    const float* __restrict__ v, float* __restrict__ out,
+                                                    float* __restrict__ lo, float* __restrict__ mo, WinDev g,
+                                                    int d, int dv, float scale, float scale_log2) {
+    constexpr int NTH = 256, ROW = 65;
+    constexpr int QI = 0, KI = D * ROW, VI = 2 * D * ROW, REGION = (2 * D + DV) * ROW;
+    constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;
+    static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
+    __shared__ float sm[REGION];
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
+    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
+    const int ax = min(max(xs, 0), W_ - 8);
+    const int sh = xs - ax;                                    // slot t <- loaded pixel t + sh
+    auto item_off = [&](int it, int C) {
+        const int yy = it & 7, f = it >> 3, yr = y0 + yy;
+        const bool ok = yy < ws && yr >= 0 && yr < H_ && f < C;
+        return ok ? (f * P_ + yr * W_ + ax) * 4 : 0x7FFFFFE0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 4));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 4));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 4));
+    u32x4 rq[NIQ][2], rk[NIQ][2], rv[NIV][2];
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        const int o = item_off(tid + NTH * j, d);
+        rq[j][0] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o, 0, 0);
+        rq[j][1] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o + 16, 0, 0);
+        rk[j][0] = __builtin_amdgcn_raw_buffer_load_b128(krs, o, 0, 0);
+        rk[j][1] = __builtin_amdgcn_raw_buffer_load_b128(krs, o + 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int o = item_off(tid + NTH * j, dv);
+        rv[j][0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, o, 0, 0);
+        rv[j][1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, o + 16, 0, 0);
+    }
+    bool valid[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) valid[t] = t < ws && xs + t >= 0 && xs + t < W_;
+    auto stage = [&](const u32x4 (&raw)[2], int it, int img) {
+        const int yy = it & 7, f = it >> 3;
+        unsigned px[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) px[t] = t < 4 ? raw[0][t] : raw[1][t - 4];
+        float* dst = sm + img + f * ROW + yy * 8;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int src = t + sh;
+            unsigned val = 0u;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) val = src == e ? px[e] : val;
+            dst[t] = valid[t] ? __uint_as_float(val) : 0.0f;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        stage(rq[j], tid + NTH * j, QI);
+        stage(rk[j], tid + NTH * j, KI);
+    }
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) stage(rv[j], tid + NTH * j, VI);
+    __syncthreads();
+
+    const int qb = wave & 1, vc = wave >> 1;
+    f32x16 sa[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int x = 0; x < 16; ++x) sa[kb][x] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < D / 2; ++t)
+            sa[kb] = mfma32x32x2(sm[KI + (2 * t + h) * ROW + kb * 32 + r], sm[QI + (2 * t + h) * ROW + qb * 32 + r], sa[kb]);
+    }
+    // mask padding key slots, exact softmax per query (lanes r and r + 32 share query r)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int kt = kb * 32 + acc_row(x, h);
+            if ((kt & 7) >= ws || (kt >> 3) >= ws) sa[kb][x] = kNegInf;
+        }
+    const float mt = swap_halves_max(lane_max<2>(sa));
+    const float mc = mt * scale_log2;
+    float ps[4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const float pr = exp2_fast(fmaf(sa[kb][x], scale_log2, -mc));
+            if (kb == 0 && x < 4) ps[x] = pr; else ps[x & 3] += pr;
+            sa[kb][x] = pr;
+        }
+    const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+    const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
+    if (vc < DV / 32) {
+        f32x16 oa;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                oa = mfma32x32x2(sm[VI + (vc * 32 + r) * ROW + kb * 32 + acc_row(x, h)], sa[kb][x], oa);
+        const int px = xs + qtx, py = y0 + qty;
+        if (qtx < ws && qty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+            const float inv = 1.0f / lt;
+            float* yb = out + (int64_t)b * dv * P_ + (int64_t)py * W_ + px;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int cc = vc * 32 + acc_row(x, h);
+                if (cc < dv) yb[(int64_t)cc * P_] = oa[x] * inv;
+            }
+        }
+    }
+    if (vc == 0 && h == 0 && qtx < ws && qty < ws) {
+        const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+        const int64_t li = qty * ws + qtx + (int64_t)g.T * wid;
+        mo[li] = mt * scale;
+        lo[li] = lt;
+    }
+}
+
+static bool rows_f32_ok(const WindowedArgs& a) {
+    return g_win_force_composed != 1 && a.dtype == FA_DTYPE_F32 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
+           a.g.ws <= 8 && a.g.S[0] >= 8 && a.d <= 64 && a.dv <= 64 &&
+           a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
+}
+
 int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default)
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
@@ -1273,6 +1419,30 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
     if (a.workspace_bytes < windowed_fwd_workspace(a.dtype, a.g, a.d, a.dv, a.batch)) {
         *why = "workspace smaller than fa_windowed_fwd_workspace()";
         return FA_ERR_WORKSPACE;
+    }
+    if constexpr (std::is_same<T, float>::value) {
+        if (rows_f32_ok(a)) {
+            const WinDev gd = to_dev(a.g);
+            const dim3 grid((unsigned)(a.g.L * a.batch));
+            const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
+#define FA_WF32(DD, DVV) hipLaunchKernelGGL((win_rows_f32<DD, DVV>), grid, dim3(256), 0, s, (const float*)a.q, \
+                                            (const float*)a.k, (const float*)a.v, (float*)a.y, a.l, a.m, gd,    \
+                                            (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e)
+            if (Dc == 32 && DVc == 32) FA_WF32(32, 32);
+            else if (Dc == 32) FA_WF32(32, 64);
+            else if (DVc == 32) FA_WF32(64, 32);
+            else FA_WF32(64, 64);
+#undef FA_WF32
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess && !fully_covered(a.g)) {
+                const int64_t total = a.g.P * a.dv * a.batch;
+                hipLaunchKernelGGL(win_nan_uncovered<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                                   (float*)a.y, (int)a.dv, total, gd);
+                e = hipGetLastError();
+            }
+            if (e != hipSuccess) { *why = hipGetErrorString(e); return FA_ERR_HIP; }
+            return FA_OK;
+        }
     }
     if constexpr (!std::is_same<T, float>::value) {
     if (fused_ok(a.dtype, a.g, a.d, a.dv)) {

@@ -99,3 +99,28 @@ def test_windowed_backward_paths(fa, geom, path):
                 assert np.all(np.isfinite(x)) and err <= 2e-2, f"path {path} d {d} dv {dv} {nm}: {err:.2e}"
     finally:
         L.fa_debug_set_win_composed(old)
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_f32_paths(fa, geom, path):
+    """fp32: the fused exact-f32 MFMA windowed kernel (path 0, stride >= ws) and
+    the composed path (1) against the float64 oracle at the fp32 tolerance."""
+    W, H, ws, st, pad = geom
+    rng = np.random.default_rng(W * 11 + H + ws)
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        for (d, dv) in DIMS:
+            B = 2
+            q, k = (rng.standard_normal((W, H, d, B)) for _ in range(2))
+            v = rng.standard_normal((W, H, dv, B))
+            y, l, m = fa.windowed_fa(*(fa.jl_tensor(a, torch.float32) for a in (q, k, v)), ws, stride=st, pad=pad)
+            torch.cuda.synchronize()
+            yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
+            tag = f"path {path} d {d} dv {dv}"
+            assert_close(_np(y), yr, "float32", f"y ({tag})", nan_ok=True)
+            assert_lm_close(_np(l), lr, "float32", f"l ({tag})")
+            assert_lm_close(_np(m), mr, "float32", f"m ({tag})")
+    finally:
+        L.fa_debug_set_win_composed(old)
