@@ -1271,6 +1271,180 @@ __global__ __launch_bounds__(256) void win_rows_f32(const float* __restrict__ q,
     }
 }
 
+// fp32 fused windowed BACKWARD (same shapes as win_rows_f32, stride >= ws so
+// dyw = dy and the fold is a direct store).  Staging as win_rows_f32 for q, k, v,
+// dy; y rows feed D = rowsum(dy ∘ y) by LDS float adds.  Phase 1, wave (qb, kb):
+// S and dP blocks (queries on accumulator rows, keys on lanes) on exact-f32 MFMA,
+// P = exp2(c (S − lse/τ)), dS = P (dP − D), both written to [query][65] LDS rows.
+// Phase 2: 12 output blocks over the 4 waves with every operand read from LDS:
+// dVᵀ = dOᵀ P, dKᵀ = τ Qᵀ dS (contraction over queries), dQᵀ = τ Kᵀ dSᵀ
+// (contraction over keys); each lane stores one slot's features to its pixel.
+template <int D, int DV>
+__global__ __launch_bounds__(256) void win_bwd_f32(const float* __restrict__ q, const float* __restrict__ k,
+                                                   const float* __restrict__ v, const float* __restrict__ y,
+                                                   const float* __restrict__ dy, const float* __restrict__ lw,
+                                                   const float* __restrict__ mw, float* __restrict__ dq,
+                                                   float* __restrict__ dk, float* __restrict__ dvo, WinDev g, int d,
+                                                   int dv, float scale, float scale_log2) {
+    constexpr int NTH = 256, ROW = 65;
+    constexpr int QI = 0, KI = D * ROW, VI = 2 * D * ROW, DOI = VI + DV * ROW, PI = DOI + DV * ROW,
+                  DSI = PI + 64 * ROW, LSEI = DSI + 64 * ROW, DI = LSEI + 64, REGION = DI + 64;
+    constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;
+    static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
+    extern __shared__ float sm[];
+    (void)REGION;
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
+    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
+    const int ax = min(max(xs, 0), W_ - 8);
+    const int sh = xs - ax;
+    const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
+    auto item_off = [&](int it, int C) {
+        const int yy = it & 7, f = it >> 3, yr = y0 + yy;
+        const bool ok = yy < ws && yr >= 0 && yr < H_ && f < C;
+        return ok ? (f * P_ + yr * W_ + ax) * 4 : 0x7FFFFFE0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 4));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 4));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 4));
+    const auto yrs = slab_rsrc(y + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 4));
+    const auto drs = slab_rsrc(dy + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 4));
+    u32x4 rq[NIQ][2], rk[NIQ][2], rv[NIV][2], rd[NIV][2], ry[NIV][2];
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        const int o = item_off(tid + NTH * j, d);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            rq[j][hh] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o + 16 * hh, 0, 0);
+            rk[j][hh] = __builtin_amdgcn_raw_buffer_load_b128(krs, o + 16 * hh, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int o = item_off(tid + NTH * j, dv);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            rv[j][hh] = __builtin_amdgcn_raw_buffer_load_b128(vrs, o + 16 * hh, 0, 0);
+            rd[j][hh] = __builtin_amdgcn_raw_buffer_load_b128(drs, o + 16 * hh, 0, 0);
+            ry[j][hh] = __builtin_amdgcn_raw_buffer_load_b128(yrs, o + 16 * hh, 0, 0);
+        }
+    }
+    if (tid < 64) {
+        const int tx = tid & 7, ty = tid >> 3;
+        float nl = kNegInf;
+        if (tx < ws && ty < ws) {
+            const int64_t li = ty * ws + tx + (int64_t)g.T * wid;
+            nl = -(mw[li] + __logf(lw[li])) / scale;
+        }
+        sm[LSEI + tid] = nl;
+        sm[DI + tid] = 0.0f;
+    }
+    bool valid[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) valid[t] = t < ws && xs + t >= 0 && xs + t < W_;
+    auto pix = [&](const u32x4 (&raw)[2], int t) {
+        const int src = t + sh;
+        unsigned val = 0u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) val = src == e ? (e < 4 ? raw[0][e] : raw[1][e - 4]) : val;
+        return valid[t] ? __uint_as_float(val) : 0.0f;
+    };
+    auto stage = [&](const u32x4 (&raw)[2], int it, int img) {
+        const int yy = it & 7, f = it >> 3;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sm[img + f * ROW + yy * 8 + t] = pix(raw, t);
+    };
+#pragma unroll
+    for (int j = 0; j < NIQ; ++j) {
+        stage(rq[j], tid + NTH * j, QI);
+        stage(rk[j], tid + NTH * j, KI);
+    }
+    __syncthreads();   // D zeroed before the adds
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) {
+        const int it = tid + NTH * j, yy = it & 7, f = it >> 3;
+        stage(rv[j], it, VI);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const float a = pix(rd[j], t), yv = pix(ry[j], t);
+            sm[DOI + f * ROW + yy * 8 + t] = a;
+            const float pr = a * yv;
+            if (pr != 0.0f) atomicAdd(&sm[DI + yy * 8 + t], pr);
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 1: S, dP blocks (qb, kb) of this wave ----
+    const int qb = wave & 1, kb = wave >> 1;
+    f32x16 sa, pa;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+        const int qs = qb * 32 + acc_row(x, h);
+        sa[x] = sm[LSEI + qs];
+        pa[x] = -sm[DI + qs];
+    }
+#pragma unroll
+    for (int t = 0; t < D / 2; ++t)
+        sa = mfma32x32x2(sm[QI + (2 * t + h) * ROW + qb * 32 + r], sm[KI + (2 * t + h) * ROW + kb * 32 + r], sa);
+#pragma unroll
+    for (int t = 0; t < DV / 2; ++t)
+        pa = mfma32x32x2(sm[DOI + (2 * t + h) * ROW + qb * 32 + r], sm[VI + (2 * t + h) * ROW + kb * 32 + r], pa);
+    const int kslot = kb * 32 + r;
+    const bool kvalid = (kslot & 7) < ws && (kslot >> 3) < ws;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+        const int qs = qb * 32 + acc_row(x, h);
+        const float pr = kvalid ? exp2_fast(sa[x] * scale_log2) : 0.0f;
+        sm[PI + qs * ROW + kslot] = pr;
+        sm[DSI + qs * ROW + kslot] = pr * pa[x];
+    }
+    __syncthreads();
+
+    // ---- phase 2 ----
+    auto store_px = [&](float* out, int C, int slot, int fbase, const f32x16& acc, float mul) {
+        const int tx = slot & 7, ty = slot >> 3, px = xs + tx, py = y0 + ty;
+        if (tx < ws && ty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+            float* ob = out + (int64_t)b * C * P_ + (int64_t)py * W_ + px;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int f = fbase + acc_row(x, h);
+                if (f < C) ob[(int64_t)f * P_] = acc[x] * mul;
+            }
+        }
+    };
+    constexpr int NDV = DV / 32 * 2, NDK = D / 32 * 2, NBLK = NDV + 2 * NDK;
+#pragma unroll
+    for (int i = 0; i < (NBLK + 3) / 4; ++i) {
+        const int blk = wave + 4 * i;
+        if (blk >= NBLK) break;
+        f32x16 acc;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
+        if (blk < NDV) {                              // dVᵀ[cb, kb2] = Σ_q dOᵀ P
+            const int cb = blk >> 1, kb2 = blk & 1;
+#pragma unroll 8
+            for (int t = 0; t < 32; ++t)
+                acc = mfma32x32x2(sm[DOI + (cb * 32 + r) * ROW + 2 * t + h], sm[PI + (2 * t + h) * ROW + kb2 * 32 + r], acc);
+            store_px(dvo, dv, kb2 * 32 + r, cb * 32, acc, 1.0f);
+        } else if (blk < NDV + NDK) {                 // dKᵀ[fb, kb2] = τ Σ_q Qᵀ dS
+            const int b2 = blk - NDV, fb = b2 >> 1, kb2 = b2 & 1;
+#pragma unroll 8
+            for (int t = 0; t < 32; ++t)
+                acc = mfma32x32x2(sm[QI + (fb * 32 + r) * ROW + 2 * t + h], sm[DSI + (2 * t + h) * ROW + kb2 * 32 + r], acc);
+            store_px(dk, d, kb2 * 32 + r, fb * 32, acc, scale);
+        } else {                                      // dQᵀ[fb, qb2] = τ Σ_key Kᵀ dSᵀ
+            const int b2 = blk - NDV - NDK, fb = b2 >> 1, qb2 = b2 & 1;
+#pragma unroll 8
+            for (int t = 0; t < 32; ++t)
+                acc = mfma32x32x2(sm[KI + (fb * 32 + r) * ROW + 2 * t + h], sm[DSI + (qb2 * 32 + r) * ROW + 2 * t + h], acc);
+            store_px(dq, d, qb2 * 32 + r, fb * 32, acc, scale);
+        }
+    }
+}
+
 static bool rows_f32_ok(const WindowedArgs& a) {
     return g_win_force_composed != 1 && a.dtype == FA_DTYPE_F32 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
            a.g.ws <= 8 && a.g.S[0] >= 8 && a.d <= 64 && a.dv <= 64 &&
@@ -1617,6 +1791,44 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
     return FA_OK;
 }
 
+static bool bwd_f32_ok(const WindowedBwdArgs& a) {
+    return g_win_force_composed != 1 && a.dtype == FA_DTYPE_F32 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
+           a.g.ws <= 8 && a.g.S[0] >= 8 && a.d <= 64 && a.dv <= 64 &&
+           a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
+}
+
+static int windowed_bwd_f32(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
+    const WinDev g = to_dev(a.g);
+    hipError_t e = hipSuccess;
+    if (!fully_covered(a.g)) {
+        if ((e = hipMemsetAsync(a.dq, 0, (size_t)(a.g.P * a.d * a.batch) * 4, s)) != hipSuccess ||
+            (e = hipMemsetAsync(a.dk, 0, (size_t)(a.g.P * a.d * a.batch) * 4, s)) != hipSuccess ||
+            (e = hipMemsetAsync(a.dv_, 0, (size_t)(a.g.P * a.dv * a.batch) * 4, s)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
+    }
+    const dim3 grid((unsigned)(a.g.L * a.batch));
+    const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
+    const size_t lds = (size_t)(2 * Dc * 65 + 2 * DVc * 65 + 2 * 64 * 65 + 128) * 4;
+#define FA_BWD_F32(DD, DVV)                                                                                     \
+    (void)hipFuncSetAttribute((const void*)win_bwd_f32<DD, DVV>, hipFuncAttributeMaxDynamicSharedMemorySize,   \
+                              (int)lds);                                                                        \
+    hipLaunchKernelGGL((win_bwd_f32<DD, DVV>), grid, dim3(256), lds, s, (const float*)a.q, (const float*)a.k,   \
+                       (const float*)a.v, (const float*)a.y, (const float*)a.dy, a.l, a.m, (float*)a.dq,        \
+                       (float*)a.dk, (float*)a.dv_, g, (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e)
+    if (Dc == 32 && DVc == 32) { FA_BWD_F32(32, 32); }
+    else if (Dc == 32) { FA_BWD_F32(32, 64); }
+    else if (DVc == 32) { FA_BWD_F32(64, 32); }
+    else { FA_BWD_F32(64, 64); }
+#undef FA_BWD_F32
+    if ((e = hipGetLastError()) != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return FA_ERR_HIP;
+    }
+    return FA_OK;
+}
+
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
         *why = "head dimension exceeds the compiled maximum (128)";
@@ -1632,6 +1844,7 @@ int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** wh
             case FA_DTYPE_F16: return windowed_bwd_rows<f16>(a, s, why);
         }
     }
+    if (bwd_f32_ok(a)) return windowed_bwd_f32(a, s, why);
     switch (a.dtype) {
         case FA_DTYPE_BF16: return windowed_bwd_typed<bf16>(a, s, why);
         case FA_DTYPE_F16: return windowed_bwd_typed<f16>(a, s, why);

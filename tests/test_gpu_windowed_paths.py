@@ -124,3 +124,31 @@ def test_windowed_f32_paths(fa, geom, path):
             assert_lm_close(_np(m), mr, "float32", f"m ({tag})")
     finally:
         L.fa_debug_set_win_composed(old)
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("geom", [g for g in GEOMS if g[3] >= g[2]], ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_backward_f32_paths(fa, geom, path):
+    """fp32 windowed backward: the fused exact-f32 MFMA kernel (path 0) and the
+    composed path (1) against the float64 oracle chain rule (fp32 tolerance)."""
+    W, H, ws, st, pad = geom
+    rng = np.random.default_rng(W * 13 + H + ws)
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        for (d, dv) in DIMS:
+            B = 2
+            q, k = (rng.standard_normal((W, H, d, B)) for _ in range(2))
+            v, dy = (rng.standard_normal((W, H, dv, B)) for _ in range(2))
+            Q, K, V, DY = (fa.jl_tensor(a, torch.float32) for a in (q, k, v, dy))
+            y, l, m = fa.windowed_fa(Q, K, V, ws, stride=st, pad=pad)
+            dq, dk, dvv = fa.windowed_fa_backward(Q, K, V, y, DY, l, m, ws, stride=st, pad=pad)
+            torch.cuda.synchronize()
+            ref = O.windowed_fa_backward(q, k, v, dy, ws, st, pad)
+            for a, b_, nm in zip((dq, dk, dvv), ref, ("dq", "dk", "dv")):
+                x = _np(a)
+                scale = max(np.abs(b_).max(), 1e-2)
+                err = np.abs(x - b_).max() / scale
+                assert np.all(np.isfinite(x)) and err <= 2e-5, f"path {path} d {d} dv {dv} {nm}: {err:.2e}"
+    finally:
+        L.fa_debug_set_win_composed(old)
