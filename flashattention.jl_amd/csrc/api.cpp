@@ -89,6 +89,14 @@ int fa_debug_set_bwd_generic(int v) {
     return old;
 }
 
+// Not part of the public header: circulant kernel override (1 one-wave-per-query,
+// 2 LDS-tiled SIMT; 0 auto).
+int fa_debug_set_circ_generic(int v) {
+    const int old = fa::g_circ_force_generic;
+    fa::g_circ_force_generic = (v == 1 || v == 2) ? v : 0;
+    return old;
+}
+
 // Not part of the public header: windowed forward path override (1 composed,
 // 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window
 // row-scatter, 5 one-window row-scatter, 6 two-window row-shift, where eligible; 0 auto).

@@ -23,8 +23,10 @@
 //    64-key tiles that intersect its own 32 bands and masks per element
 //    (0 <= u − r − off < W) only on tiles that are not inside every band.
 //    Roofline: HBM for W below ≈600 (intensity ≈ W/2 FLOP/B).
-//  * circ_fwd_generic (every dtype incl. fp32, any N / alignment): one wave per
-//    query, exact online softmax in fp32, lanes over features.
+//  * circ_fwd_simt (every dtype incl. fp32, any N / alignment): one thread per
+//    query, LDS-tiled key union, exact fp32 arithmetic (below).
+//  * circ_fwd_generic: one wave per query, lanes over features — kept only as a
+//    reference path behind fa_debug_set_circ_generic.
 #include <type_traits>
 
 #include "fa_common.h"
@@ -32,6 +34,8 @@
 #include "../../include/fa_hip.h"
 
 namespace fa {
+
+int g_circ_force_generic = 0;   // debug knob: 1 = one-wave-per-query kernel, 2 = LDS-tiled SIMT kernel (non-MFMA shapes)
 
 struct CircParams {
     const void* Q;
@@ -95,6 +99,110 @@ __global__ __launch_bounds__(256) void circ_fwd_generic(CircParams P) {
         if (cc < dv) O[(int64_t)cc * N + i] = (T)(acc[u] / l);
     }
     if (lane == 0) {
+        P.m[(int64_t)b * N + i] = m * P.scale;
+        P.l[(int64_t)b * N + i] = l;
+    }
+}
+
+// --------------------------------------------------------------------------
+// LDS-tiled SIMT kernel (every dtype incl. fp32, any N / alignment): one thread
+// per query, 256 consecutive queries per workgroup.  The union of their bands,
+// 256 + W − 1 consecutive circular key positions, streams through LDS in tiles
+// of KT keys stored [key][feature] (fp32, rows padded by 4 floats: the per-lane
+// float4 reads of different keys hit distinct banks).  Each lane scores its
+// in-band keys (exact fp32 dot products) with the lazy online rescale of the
+// MFMA kernels (threshold 2^8) and accumulates O in registers.  Tiles outside a
+// wave's band union are skipped.
+// Replaces one-wave-per-query: ragged N (16383) 35.7 ms -> ~1 ms, fp32 likewise.
+// --------------------------------------------------------------------------
+template <class T, int D, int DV, int KT>
+__global__ __launch_bounds__(256) void circ_fwd_simt(CircParams P) {
+    constexpr int DR = D + 4, VR = DV + 4;
+    __shared__ __attribute__((aligned(16))) float sk[KT * DR], sv[KT * VR];
+    const int N = P.N, d = P.d, dv = P.dv, W = P.W;
+    const int nq = (N + 255) / 256;
+    const int lid = xcd_remap(blockIdx.x, P.total_wg);
+    const int b = lid / nq, q0 = (lid - b * nq) * 256;
+    const int tid = threadIdx.x, r = tid, i = q0 + tid;
+    const T* Qb = (const T*)P.Q + (int64_t)b * N * d;
+    const T* Kb = (const T*)P.K + (int64_t)b * N * d;
+    const T* Vb = (const T*)P.V + (int64_t)b * N * dv;
+    float qv[D], o[DV];
+#pragma unroll
+    for (int f = 0; f < D; ++f) qv[f] = (i < N && f < d) ? (float)Qb[(int64_t)f * N + i] : 0.0f;
+#pragma unroll
+    for (int f = 0; f < DV; ++f) o[f] = 0.0f;
+    const float c = P.scale_log2;
+    const float thr_raw = kRescaleLog2 / c;
+    float m_used = kNegInf, m_true = kNegInf, l = 0.0f;
+    const int U = 256 + W - 1;
+    const int ntile = (U + KT - 1) / KT;
+    const int base = ((q0 - P.p) % N + N) % N;        // union position u <-> key (base + u) mod N
+    const int w0 = tid & ~63;                          // this wave's band union: u in [w0, w0 + 63 + W - 1]
+    for (int tt = 0; tt < ntile; ++tt) {
+        const int u0 = tt * KT;
+        __syncthreads();
+        // stage KT keys x features (consecutive threads -> consecutive keys: coalesced)
+        for (int e = tid; e < KT * D; e += 256) {
+            const int kk = e % KT, f = e / KT;
+            const int key = (int)(((int64_t)base + u0 + kk) % N);
+            sk[kk * DR + f] = f < d ? (float)Kb[(int64_t)f * N + key] : 0.0f;
+        }
+        for (int e = tid; e < KT * DV; e += 256) {
+            const int kk = e % KT, f = e / KT;
+            const int key = (int)(((int64_t)base + u0 + kk) % N);
+            sv[kk * VR + f] = f < dv ? (float)Vb[(int64_t)f * N + key] : 0.0f;
+        }
+        __syncthreads();
+        if (u0 + KT <= w0 || u0 > w0 + 63 + W - 1) continue;   // wave-uniform
+#pragma unroll 2
+        for (int kk = 0; kk < KT; ++kk) {
+            const int u = u0 + kk;
+            if (u < r || u >= r + W) continue;
+            const float4* kr = (const float4*)(sk + kk * DR);
+            float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+            for (int f4 = 0; f4 < D / 4; ++f4) {
+                const float4 kv = kr[f4];
+                a0 = fmaf(qv[4 * f4], kv.x, a0);
+                a1 = fmaf(qv[4 * f4 + 1], kv.y, a1);
+                a0 = fmaf(qv[4 * f4 + 2], kv.z, a0);
+                a1 = fmaf(qv[4 * f4 + 3], kv.w, a1);
+            }
+            const float sc = a0 + a1;
+            m_true = vmax(m_true, sc);
+            if (sc > m_used + thr_raw) {               // lazy rescale (rare; always on the first key)
+                const float a = exp2_fast((m_used - sc) * c);
+                l *= a;
+#pragma unroll
+                for (int f = 0; f < DV; ++f) o[f] *= a;
+                m_used = sc;
+            }
+            const float pr = exp2_fast((sc - m_used) * c);
+            l += pr;
+            const float4* vr = (const float4*)(sv + kk * VR);
+#pragma unroll
+            for (int f4 = 0; f4 < DV / 4; ++f4) {
+                const float4 vv = vr[f4];
+                o[4 * f4] = fmaf(pr, vv.x, o[4 * f4]);
+                o[4 * f4 + 1] = fmaf(pr, vv.y, o[4 * f4 + 1]);
+                o[4 * f4 + 2] = fmaf(pr, vv.z, o[4 * f4 + 2]);
+                o[4 * f4 + 3] = fmaf(pr, vv.w, o[4 * f4 + 3]);
+            }
+        }
+    }
+    // l, O are relative to 2^(c·m_used); the returned l is relative to the exact max
+    l *= exp2_fast((m_used - m_true) * c);
+    const float osc = exp2_fast((m_used - m_true) * c);
+#pragma unroll
+    for (int f = 0; f < DV; ++f) o[f] *= osc;
+    const float m = m_true;
+    if (i < N) {
+        T* Ob = (T*)P.O + (int64_t)b * N * dv;
+        const float inv = 1.0f / l;
+#pragma unroll
+        for (int f = 0; f < DV; ++f)
+            if (f < dv) Ob[(int64_t)f * N + i] = (T)(o[f] * inv);
         P.m[(int64_t)b * N + i] = m * P.scale;
         P.l[(int64_t)b * N + i] = l;
     }
@@ -335,9 +443,22 @@ static void launch_circ_typed(CircParams p, int64_t batch, bool fast, hipStream_
             return;
         }
     }
-    p.total_wg = (int)batch;   // generic kernel: slab count
-    const int64_t waves = (int64_t)p.N * batch;
-    hipLaunchKernelGGL((circ_fwd_generic<T>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
+    // small grids (< 128 workgroups of 256 queries) keep one wave per query: more
+    // parallelism there (N 4096, d 32, one slab, W 129 fp32: 72 vs 137 us)
+    if (g_circ_force_generic == 1 || (g_circ_force_generic != 2 && (int64_t)(p.N + 255) / 256 * batch < 128)) {
+        p.total_wg = (int)batch;   // one-wave-per-query kernel: slab count
+        const int64_t waves = (int64_t)p.N * batch;
+        hipLaunchKernelGGL((circ_fwd_generic<T>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
+        return;
+    }
+    p.total_wg = (int)((p.N + 255) / 256 * batch);
+    const dim3 grid((unsigned)p.total_wg);
+    const int Dc = head_dim_class(p.d), DVc = head_dim_class(p.dv);
+#define FA_CS(DD, DVV, KTT) hipLaunchKernelGGL((circ_fwd_simt<T, DD, DVV, KTT>), grid, dim3(256), 0, s, p)
+    if (Dc <= 32 && DVc <= 32) FA_CS(32, 32, 32);
+    else if (Dc <= 64 && DVc <= 64) FA_CS(64, 64, 32);
+    else FA_CS(128, 128, 8);
+#undef FA_CS
 }
 
 int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why) {
@@ -358,7 +479,7 @@ int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why) {
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
     const bool fast = a.dtype != FA_DTYPE_F32 && a.N % 8 == 0 && circ_aligned16(a.K) && circ_aligned16(a.V) &&
-                      ((a.N + 127) / 128) * a.batch <= INT32_MAX;
+                      ((a.N + 127) / 128) * a.batch <= INT32_MAX && g_circ_force_generic == 0;
     switch (a.dtype) {
         case FA_DTYPE_BF16: launch_circ_typed<bf16>(p, a.batch, fast, s); break;
         case FA_DTYPE_F16: launch_circ_typed<f16>(p, a.batch, fast, s); break;

@@ -112,5 +112,6 @@ constexpr int kMaxHeadDim = 128;
 extern int g_fwd_variant;       // forward kernel variant (debug/benchmark knob)
 extern int g_bwd_force_generic; // backward: force the generic SIMT path (debug knob)
 extern int g_win_force_composed; // windowed: force the composed gather/dense/fold path (debug knob)
+extern int g_circ_force_generic; // circulant: force the one-wave-per-query kernel (debug knob)
 
 }  // namespace fa

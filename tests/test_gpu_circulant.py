@@ -125,3 +125,34 @@ def test_circulant_full_size_band_property(fa):
         assert torch.allclose(m[:, 0, b], mm, rtol=1e-4, atol=1e-4)
         assert torch.allclose(l[:, 0, b], ll, rtol=1e-4)
     assert torch.isfinite(o.float()).all()
+
+
+@pytest.mark.parametrize("N,d,dv,W,dtype", [(100, 32, 16, 9, "float32"), (257, 64, 64, 129, "bfloat16"),
+                                            (30, 12, 6, 7, "float16"), (64, 128, 96, 65, "float32"),
+                                            (1000, 64, 32, 1001, "bfloat16"), (5, 8, 8, 12, "float32")])
+def test_circulant_simt_vs_reference_kernel(fa, N, d, dv, W, dtype):
+    """The LDS-tiled SIMT kernel (fp32 / ragged N) against the oracle and
+    against the one-wave-per-query reference kernel on the same inputs."""
+    tdt = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}[dtype]
+    rng = np.random.default_rng(N + W + d)
+    cast = lambda a: torch.tensor(a).to(tdt).double().numpy()
+    q, k = cast(rng.standard_normal((N, d, 2))), cast(rng.standard_normal((N, d, 2)))
+    v = cast(rng.standard_normal((N, dv, 2)))
+    Q, K, V = (fa.jl_tensor(a, tdt) for a in (q, k, v))
+    L = fa.lib()
+    L.fa_debug_set_circ_generic(2)          # force the SIMT kernel (small grids pick the other)
+    try:
+        o1, l1, m1 = fa.circulant_fa(Q, K, V, W)
+    finally:
+        L.fa_debug_set_circ_generic(0)
+    L.fa_debug_set_circ_generic(1)
+    try:
+        o2, l2, m2 = fa.circulant_fa(Q, K, V, W)
+    finally:
+        L.fa_debug_set_circ_generic(0)
+    torch.cuda.synchronize()
+    orr, lr, mr = O.circulant_fa3(q, k, v, W)
+    assert_close(_np(o1), orr, dtype, "O")
+    assert_lm_close(_np(l1), lr, dtype, "l")
+    assert_lm_close(_np(m1), mr, dtype, "m")
+    assert_close(_np(o1), _np(o2), dtype, "O simt vs one-wave")
