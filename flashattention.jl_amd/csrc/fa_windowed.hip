@@ -1553,14 +1553,16 @@ size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t
     const size_t tok = (size_t)(g.T * g.L * batch);
     if (fused_ok(dtype, g, d, dv))   // direct (no overlap): nothing; overlap: the window outputs
         return g.stride >= g.ws ? 0 : align256(tok * dv * esize(dtype)) + 256;
-    return align256(tok * d * esize(dtype)) * 2 + align256(tok * dv * esize(dtype)) * 2 + 256;
+    return align256(tok * d * esize(dtype)) * 2 + align256(tok * dv * esize(dtype)) * 2 +
+           align256(dense_fwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) + 256;
 }
 
 size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
     const size_t tok = (size_t)(g.T * g.L * batch);
     const size_t e = esize(dtype);
     return align256(tok * d * e) * 4 + align256(tok * dv * e) * 4 + align256(tok * 4) * 2 +
-           align256(dense_bwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) + 256;
+           align256(dense_bwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) +
+           align256(dense_fwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) + 256;
 }
 
 template <class T>
@@ -1645,7 +1647,7 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
     void* qw = ws;  ws += align256(tok * a.d * sizeof(T));
     void* kw = ws;  ws += align256(tok * a.d * sizeof(T));
     void* vw = ws;  ws += align256(tok * a.dv * sizeof(T));
-    void* ow = ws;
+    void* ow = ws;  ws += align256(tok * a.dv * sizeof(T));
     hipError_t e;
     if ((e = gather<T>(a.q, qw, (int)a.d, a.batch, g, false, s)) != hipSuccess ||
         (e = gather<T>(a.k, kw, (int)a.d, a.batch, g, false, s)) != hipSuccess ||
@@ -1653,7 +1655,11 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
         *why = hipGetErrorString(e);
         return FA_ERR_HIP;
     }
+    // the window batch has T = ws^k tokens (49 at ws 7): the dense workspace lets
+    // the fast kernels run on padded key copies (or split-KV) instead of the generic one
     DenseArgs da{a.dtype, qw, kw, vw, ow, a.l, a.m, a.g.T, a.g.T, a.d, a.dv, a.g.L * a.batch, a.scale};
+    da.workspace = ws;
+    da.workspace_bytes = dense_fwd_workspace(a.dtype, a.g.T, a.g.T, a.d, a.dv, a.g.L * a.batch);
     const int rc = launch_dense_fwd(da, s, why);
     if (rc != FA_OK) return rc;
     if ((e = fold<T>(ow, a.y, (int)a.dv, a.batch, g, true, s)) != hipSuccess) {
@@ -1730,6 +1736,8 @@ static int windowed_bwd_typed(const WindowedBwdArgs& a, hipStream_t s, const cha
     float* mw = (float*)take(tok * 4);
     const size_t dws = dense_bwd_workspace(a.dtype, a.g.T, a.g.T, a.d, a.dv, nb);
     void* dwork = take(dws);
+    const size_t fws = dense_fwd_workspace(a.dtype, a.g.T, a.g.T, a.d, a.dv, nb);
+    void* fwork = take(fws);
     hipError_t e;
     if ((e = gather<T>(a.q, qw, (int)a.d, a.batch, g, false, s)) != hipSuccess ||
         (e = gather<T>(a.k, kw, (int)a.d, a.batch, g, false, s)) != hipSuccess ||
@@ -1740,6 +1748,8 @@ static int windowed_bwd_typed(const WindowedBwdArgs& a, hipStream_t s, const cha
     }
     // per-window outputs O_w (the backward's D = rowsum(dO_w ∘ O_w) needs them)
     DenseArgs da{a.dtype, qw, kw, vw, ow, lw, mw, a.g.T, a.g.T, a.d, a.dv, nb, a.scale};
+    da.workspace = fwork;
+    da.workspace_bytes = fws;
     int rc = launch_dense_fwd(da, s, why);
     if (rc != FA_OK) return rc;
     DenseBwdArgs ba{a.dtype, qw, kw, vw, ow, dyw, a.l, a.m, dqw, dkw, dvw, a.g.T, a.g.T, a.d, a.dv, nb,
