@@ -887,8 +887,9 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
 
     // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
     const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
-    if (vc < DV / 32 && w.ok) {
-        const char* vimg = wsm + 2 * QIMG + (vc * 32 + r) * VROW + 16 * h;
+#pragma unroll
+    for (int cv = vc; cv < DV / 32 && w.ok; cv += 2) {   // DV = 128: chunks vc and vc + 2
+        const char* vimg = wsm + 2 * QIMG + (cv * 32 + r) * VROW + 16 * h;
         f32x16 oa;
 #pragma unroll
         for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
@@ -902,7 +903,7 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
             T* yb = out + (int64_t)w.b * dv * P_ + (int64_t)py * W_ + px;
 #pragma unroll
             for (int x = 0; x < 16; ++x) {
-                const int cc = vc * 32 + acc_row(x, h);
+                const int cc = cv * 32 + acc_row(x, h);
                 if (cc < dv) yb[(int64_t)cc * P_] = (T)(oa[x] * inv);
             }
         }
@@ -1514,6 +1515,17 @@ static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStr
     return hipGetLastError();
 }
 
+// d or dv in (64, 128] (bf16/f16, 2-D, non-overlapping, ws <= 7, width % 8 == 0,
+// 16-B aligned): the one-window row-shift kernel at 128 features (50 KB of LDS,
+// every wave runs two of the four 32-feature output chunks).  The workspace
+// query cannot see the pointers, so it keeps the composed path's size.
+static bool rows128_ok(const WindowedArgs& a) {
+    return g_win_force_composed != 1 && g_win_force_composed != 2 && a.dtype != FA_DTYPE_F32 &&
+           (a.d > 64 || a.dv > 64) && a.d <= 128 && a.dv <= 128 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
+           a.g.ws <= 7 && a.g.S[0] % 8 == 0 && ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 &&
+           ((uintptr_t)a.v & 15u) == 0 && a.g.P * 128 * 2 < INT32_MAX;
+}
+
 template <class T, int D, int DV>
 static hipError_t launch_rows_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
     const int ngx = (int)((a.g.O[0] + 3) / 4);
@@ -1621,6 +1633,21 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
         }
     }
     if constexpr (!std::is_same<T, float>::value) {
+    if (rows128_ok(a)) {
+        const int64_t nw = a.g.L * a.batch;
+        hipLaunchKernelGGL((win_rows1s<T, 128, 128, 1>), dim3((unsigned)nw), dim3(256), 0, s, (const T*)a.q,
+                           (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, nw, a.scale,
+                           a.scale * kLog2e);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess && !fully_covered(a.g)) {
+            const int64_t total = a.g.P * a.dv * a.batch;
+            hipLaunchKernelGGL(win_nan_uncovered<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                               (T*)a.y, (int)a.dv, total, g);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) { *why = hipGetErrorString(e); return FA_ERR_HIP; }
+        return FA_OK;
+    }
     if (fused_ok(a.dtype, a.g, a.d, a.dv)) {
         hipError_t e;
         if (a.g.stride >= a.g.ws) {
@@ -1770,8 +1797,8 @@ static bool bwd_rows_ok(const WindowedBwdArgs& a) {
     const bool al = ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 && ((uintptr_t)a.v & 15u) == 0 &&
                     ((uintptr_t)a.y & 15u) == 0 && ((uintptr_t)a.dy & 15u) == 0;
     return g_win_force_composed != 1 && a.dtype != FA_DTYPE_F32 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
-           a.g.ws <= 7 && a.g.S[0] % 8 == 0 && a.d <= 64 && a.dv <= 64 && al &&
-           a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX;
+           a.g.ws <= 7 && a.g.S[0] % 8 == 0 && a.d <= 128 && a.dv <= 128 && al &&
+           a.g.P * 128 * 2 < INT32_MAX;
 }
 
 template <class T>
@@ -1789,7 +1816,8 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
     const dim3 grid((unsigned)(a.g.L * a.batch));
 #define FA_BWD_ROWS(DD, DVV)                                                                                 hipLaunchKernelGGL((win_bwd_rows<T, DD, DVV>), grid, dim3(256), 0, s, (const T*)a.q, (const T*)a.k,                         (const T*)a.v, (const T*)a.y, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk,                              (T*)a.dv_, g, (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e)
     const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
-    if (Dc == 32 && DVc == 32) FA_BWD_ROWS(32, 32);
+    if (a.d > 64 || a.dv > 64) FA_BWD_ROWS(128, 128);   // 83 KB of LDS: one workgroup per CU
+    else if (Dc == 32 && DVc == 32) FA_BWD_ROWS(32, 32);
     else if (Dc == 32) FA_BWD_ROWS(32, 64);
     else if (DVc == 32) FA_BWD_ROWS(64, 32);
     else FA_BWD_ROWS(64, 64);

@@ -69,13 +69,44 @@ def test_windowed_forced_path(fa, geom, path):
         L.fa_debug_set_win_composed(old)
 
 
+DIMS128 = [(128, 128), (96, 64), (64, 128), (128, 40)]
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_wide_heads(fa, geom, path):
+    """d or dv in (64, 128]: path 0 runs the one-window row-shift kernel at 128
+    features where the geometry allows (stride >= ws, ws <= 7), the composed
+    path otherwise; path 1 forces the composed path.  Same oracle."""
+    W, H, ws, st, pad = geom
+    rng = np.random.default_rng(W * 977 + H * 13 + ws)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        for (d, dv) in DIMS128:
+            B = 2
+            q, k = (bf(rng.standard_normal((W, H, d, B))) for _ in range(2))
+            v = bf(rng.standard_normal((W, H, dv, B)))
+            y, l, m = fa.windowed_fa(*(fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v)), ws,
+                                     stride=st, pad=pad)
+            torch.cuda.synchronize()
+            yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
+            tag = f"path {path} d {d} dv {dv}"
+            assert_close(_np(y), yr, "bfloat16", f"y ({tag})", nan_ok=True)
+            assert_lm_close(_np(l), lr, "bfloat16", f"l ({tag})")
+            assert_lm_close(_np(m), mr, "bfloat16", f"m ({tag})")
+    finally:
+        L.fa_debug_set_win_composed(old)
+
+
 BWD_GEOMS = [g for g in GEOMS if g[3] >= g[2] and g[2] <= 7]   # stride >= ws, ws <= 7: the fused backward
 
 
 @pytest.mark.parametrize("path", [0, 1])
 @pytest.mark.parametrize("geom", BWD_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
 def test_windowed_backward_paths(fa, geom, path):
-    """Fused windowed backward (path 0: win_bwd_rows) and the composed
+    """Fused windowed backward (path 0: win_bwd_rows, 64- or 128-feature class) and the composed
     gather → dense backward → fold path (1) vs the oracle chain rule."""
     W, H, ws, st, pad = geom
     rng = np.random.default_rng(W * 7 + H * 3 + ws)
@@ -83,7 +114,7 @@ def test_windowed_backward_paths(fa, geom, path):
     L = fa.lib()
     old = L.fa_debug_set_win_composed(path)
     try:
-        for (d, dv) in DIMS:
+        for (d, dv) in DIMS + DIMS128:   # d, dv > 64: the fused kernel at 128 features
             B = 2
             q, k = (bf(rng.standard_normal((W, H, d, B))) for _ in range(2))
             v, dy = (bf(rng.standard_normal((W, H, dv, B))) for _ in range(2))
