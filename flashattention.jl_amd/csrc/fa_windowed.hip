@@ -958,6 +958,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     float* const lse_s = (float*)(smem + OLSE);   // −lse/τ per query slot (raw score units)
     float* const dsum = (float*)(smem + OD);      // D per query slot
 
+    FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
@@ -1022,6 +1023,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         *(u32x4*)(smem + OK_ + o) = shift_row(rk[j], sh, mask);
     }
     lds_barrier();   // dsum zeroed before the adds below
+    FA_STAMP(1);
 #pragma unroll
     for (int j = 0; j < NIV; ++j) {
         const int it = tid + NTH * j, o = koff(it), yy = it & 7;
@@ -1037,6 +1039,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         }
     }
     __syncthreads();
+    FA_STAMP(2);
 
     // ---- phase 1: S and dP blocks (qb, kb) of this wave ----
     const int qb = wave & 1, kb = wave >> 1;
@@ -1078,6 +1081,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         *(typename Frag8<T>::half*)(smem + ODS + o) = s4;
     }
     lds_barrier();
+    FA_STAMP(3);
 
     // ---- phase 2: dVᵀ, dKᵀ, dQᵀ blocks ----
     // row read: 8 consecutive slots 16 s + 8 h of feature row f of a [feature][slot] image
@@ -1130,6 +1134,8 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
             store_px(dq, d, qb2 * 32 + r, fb * 32, acc, scale);
         }
     }
+    FA_STAMP(4);
+    FA_STAMP(5);
 }
 
 // --------------------------------------------------------------------------
