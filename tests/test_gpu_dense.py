@@ -276,3 +276,26 @@ def test_forward_split_kv(fa, N, Nk, d, dv, B):
     assert_close(_np(y1), _np(y2), "bfloat16", "y split vs unsplit")
     assert np.array_equal(_np(m1), _np(m2)), "m is the exact row max either way"
     assert_lm_close(_np(l1), _np(l2), "bfloat16", "l split vs unsplit")
+
+
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("N,Nk,d,dv,B,dtype", [(300, 200, 64, 64, 2, "bfloat16"), (513, 4100, 64, 32, 1, "bfloat16"),
+                                               (256, 320, 128, 128, 2, "bfloat16"), (100, 72, 32, 64, 3, "float16"),
+                                               (77, 136, 128, 64, 1, "float16"), (1024, 1024, 96, 96, 1, "bfloat16")])
+def test_forced_forward_variants(fa, variant, N, Nk, d, dv, B, dtype):
+    """Every fast-kernel geometry (fa_debug_set_fwd_variant: 32x32x16 MFMA 4..7,
+    16x16x32 MFMA 8, 9) against the oracle, ragged Nk and dv != d included."""
+    L = fa.lib()
+    rng = np.random.default_rng(N * 7 + Nk + d * 3 + dv)
+    cast = lambda a: torch.tensor(a).to(DT[dtype]).double().numpy()
+    q, k, v = cast(rng.standard_normal((N, d, B))), cast(rng.standard_normal((Nk, d, B))), cast(rng.standard_normal((Nk, dv, B)))
+    old = L.fa_debug_set_fwd_variant(variant)
+    try:
+        y, l, m = fa.dense_fa(*(fa.jl_tensor(a, DT[dtype]) for a in (q, k, v)))
+        torch.cuda.synchronize()
+    finally:
+        L.fa_debug_set_fwd_variant(old)
+    yr, lr, mr = O.dense_fa3(q, k, v)
+    assert_close(_np(y), yr, dtype, f"y variant {variant}")
+    assert_lm_close(_np(l), lr, dtype, "l")
+    assert_lm_close(_np(m), mr, dtype, "m")
