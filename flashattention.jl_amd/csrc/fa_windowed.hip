@@ -950,13 +950,13 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     constexpr int NTH = 256, KROW = 128, PROW = 144;
     constexpr int QIMG = D * KROW, VIMG = DV * KROW, PIMG = 64 * PROW;
     constexpr int OQ = 0, OK_ = QIMG, OV = 2 * QIMG, ODO = 2 * QIMG + VIMG, OP = 2 * QIMG + 2 * VIMG,
-                  ODS = OP + PIMG, OLSE = ODS + PIMG, OD = OLSE + 256, REGION = OD + 256;
+                  ODS = OP + PIMG, OLSE = ODS + PIMG, OD = OLSE + 256, REGION = OD + 4 * 256;
     constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;
     static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
     __shared__ __attribute__((aligned(16))) char smem[REGION];
     auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
     float* const lse_s = (float*)(smem + OLSE);   // −lse/τ per query slot (raw score units)
-    float* const dsum = (float*)(smem + OD);      // D per query slot
+    float* const dsum = (float*)(smem + OD);      // D per query slot: one partial per wave [4][64]
 
     FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -993,7 +993,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         rd[j] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
         ry[j] = __builtin_amdgcn_raw_buffer_load_b128(yrs, o, 0, 0);
     }
-    // per-slot constants: −lse/τ (+inf lse outside the window) and D = 0
+    // per-slot constant −lse/τ (+inf lse outside the window)
     if (tid < 64) {
         const int tx = tid & 7, ty = tid >> 3;
         float nl = kNegInf;
@@ -1002,7 +1002,6 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
             nl = -(mw[li] + __logf(lw[li])) / scale;
         }
         lse_s[tid] = nl;
-        dsum[tid] = 0.0f;
     }
     unsigned mask[4];
 #pragma unroll
@@ -1022,11 +1021,17 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         *(u32x4*)(smem + OQ + o) = shift_row(rq[j], sh, mask);
         *(u32x4*)(smem + OK_ + o) = shift_row(rk[j], sh, mask);
     }
-    lds_barrier();   // dsum zeroed before the adds below
     FA_STAMP(1);
+    // D = rowsum(dy ∘ y) per slot.  Lane (8·fl + yy) of wave w holds window row yy of
+    // features 8w + 32j + fl: sum over j in registers, over fl (lane bits 3..5) by
+    // row_ror:8 + permlane16/32 swaps, then lanes 0..7 write the wave's partial for
+    // the 8 slots of their row (no LDS atomics: same-address adds serialise).
+    float dp[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dp[e] = 0.0f;
 #pragma unroll
     for (int j = 0; j < NIV; ++j) {
-        const int it = tid + NTH * j, o = koff(it), yy = it & 7;
+        const int it = tid + NTH * j, o = koff(it);
         const u32x4 dd = shift_row(rd[j], sh, mask), yv = shift_row(ry[j], sh, mask);
         *(u32x4*)(smem + OV + o) = shift_row(rv[j], sh, mask);
         *(u32x4*)(smem + ODO + o) = dd;
@@ -1034,9 +1039,21 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         for (int e = 0; e < 8; ++e) {
             const unsigned short a16 = (unsigned short)((e & 1) ? (dd[e >> 1] >> 16) : (dd[e >> 1] & 0xFFFFu));
             const unsigned short b16 = (unsigned short)((e & 1) ? (yv[e >> 1] >> 16) : (yv[e >> 1] & 0xFFFFu));
-            const float pr = (float)__builtin_bit_cast(T, a16) * (float)__builtin_bit_cast(T, b16);
-            if (pr != 0.0f) atomicAdd(&dsum[yy * 8 + e], pr);
+            dp[e] = fmaf((float)__builtin_bit_cast(T, a16), (float)__builtin_bit_cast(T, b16), dp[e]);
         }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        float x = dp[e];
+        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
+        auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+        auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        dp[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+    }
+    if (lane < 8) {
+        *(f32x4*)(dsum + wave * 64 + lane * 8) = f32x4{dp[0], dp[1], dp[2], dp[3]};
+        *(f32x4*)(dsum + wave * 64 + lane * 8 + 4) = f32x4{dp[4], dp[5], dp[6], dp[7]};
     }
     __syncthreads();
     FA_STAMP(2);
@@ -1056,7 +1073,8 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     for (int x4 = 0; x4 < 4; ++x4) {
         const int qrow = qb * 32 + acc_row(4 * x4, h);
         const f32x4 l4 = *(const f32x4*)(lse_s + qrow);
-        const f32x4 d4 = *(const f32x4*)(dsum + qrow);
+        const f32x4 d4 = (*(const f32x4*)(dsum + qrow) + *(const f32x4*)(dsum + 64 + qrow)) +
+                         (*(const f32x4*)(dsum + 128 + qrow) + *(const f32x4*)(dsum + 192 + qrow));
 #pragma unroll
         for (int e = 0; e < 4; ++e) { sa[4 * x4 + e] = l4[e]; pa[4 * x4 + e] = -d4[e]; }
     }
