@@ -35,6 +35,23 @@ float resolve_scale(float scale, int64_t d) {
     return scale;
 }
 
+// Empty inputs, as dense_fa! (src/dense.jl:21-102) treats them: N = 0 or batch = 0
+// runs no tile (nothing to write); Nk = 0 leaves the initial O = 0, l = 0,
+// m = −Inf (:58-60).  Returns true when the call is complete.
+bool dense_fwd_empty(int dtype, void* O, float* l, float* m, int64_t N, int64_t Nk, int64_t dv, int64_t batch,
+                     hipStream_t s, int* rc) {
+    *rc = FA_OK;
+    if (N == 0 || batch == 0) return true;
+    if (Nk != 0) return false;
+    const size_t esz = dtype == FA_DTYPE_F32 ? 4 : 2;
+    if (!O || !l || !m) { *rc = FA_ERR_INVALID_ARG; return true; }
+    if (hipMemsetAsync(O, 0, (size_t)(N * dv * batch) * esz, s) != hipSuccess ||
+        hipMemsetAsync(l, 0, (size_t)(N * batch) * 4, s) != hipSuccess ||
+        hipMemsetD32Async((hipDeviceptr_t)m, 0xFF800000u, (size_t)(N * batch), s) != hipSuccess)
+        *rc = FA_ERR_HIP;
+    return true;
+}
+
 // Window geometry of NNlib.unfold(x, (ws…, d, 1); stride, pad) (src/utils.jl:40).
 int make_geom(fa::WindowGeom& g, int nspatial, const int64_t* spatial, int64_t ws, int64_t stride,
               int64_t pad, const char** why) {
@@ -117,8 +134,11 @@ int fa_dense_fwd_ws(int dtype, const void* Q, const void* K, const void* V, void
                     void* workspace, size_t workspace_bytes, void* hip_stream) {
     static const char* fn = "fa_dense_fwd_ws";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, d, dv, batch must be >= 1");
+    if (N < 0 || Nk < 0 || d < 1 || dv < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, batch must be >= 0 and d, dv >= 1");
+    int erc;
+    if (dense_fwd_empty(dtype, O, l, m, N, Nk, dv, batch, (hipStream_t)hip_stream, &erc))
+        return erc == FA_OK ? ok() : fail(erc, fn, erc == FA_ERR_HIP ? "hipMemsetAsync failed" : "null pointer");
     if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     const size_t need = fa::dense_fwd_workspace(dtype, N, Nk, d, dv, batch);
     if (need > 0 && (!workspace || workspace_bytes < need))
@@ -136,8 +156,11 @@ int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O
                  void* hip_stream) {
     static const char* fn = "fa_dense_fwd";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, d, dv, batch must be >= 1");
+    if (N < 0 || Nk < 0 || d < 1 || dv < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, batch must be >= 0 and d, dv >= 1");
+    int erc;
+    if (dense_fwd_empty(dtype, O, l, m, N, Nk, dv, batch, (hipStream_t)hip_stream, &erc))
+        return erc == FA_OK ? ok() : fail(erc, fn, erc == FA_ERR_HIP ? "hipMemsetAsync failed" : "null pointer");
     if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     fa::DenseArgs a{dtype, Q, K, V, O, l, m, N, Nk, d, dv, batch, resolve_scale(scale, d)};
     const char* why = "";
@@ -156,8 +179,19 @@ int fa_dense_bwd(int dtype, const void* Q, const void* K, const void* V, const v
                  size_t workspace_bytes, void* hip_stream) {
     static const char* fn = "fa_dense_bwd";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, d, dv, batch must be >= 1");
+    if (N < 0 || Nk < 0 || d < 1 || dv < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, batch must be >= 0 and d, dv >= 1");
+    if (N == 0 || Nk == 0 || batch == 0) {   // empty sums: every gradient element is 0
+        const size_t esz = dtype == FA_DTYPE_F32 ? 4 : 2;
+        const hipStream_t s = (hipStream_t)hip_stream;
+        const size_t nq = (size_t)(N * d * batch), nk = (size_t)(Nk * d * batch), nv = (size_t)(Nk * dv * batch);
+        if ((nq && !dQ) || (nk && (!dK || !dV))) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+        if ((nq && hipMemsetAsync(dQ, 0, nq * esz, s) != hipSuccess) ||
+            (nk && hipMemsetAsync(dK, 0, nk * esz, s) != hipSuccess) ||
+            (nv && hipMemsetAsync(dV, 0, nv * esz, s) != hipSuccess))
+            return fail(FA_ERR_HIP, fn, "hipMemsetAsync failed");
+        return ok();
+    }
     if (!Q || !K || !V || !O || !dO || !l || !m || !dQ || !dK || !dV)
         return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     const size_t need = fa::dense_bwd_workspace(dtype, N, Nk, d, dv, batch);

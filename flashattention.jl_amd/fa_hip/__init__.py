@@ -162,7 +162,10 @@ def jl_strides(shape: Sequence[int]) -> Tuple[int, ...]:
 
 
 def is_jl_contiguous(t: torch.Tensor) -> bool:
-    """True if ``t`` is laid out like a Julia Array of the same shape."""
+    """True if ``t`` is laid out like a Julia Array of the same shape (an empty
+    array trivially is: no element is ever addressed)."""
+    if t.numel() == 0:
+        return True
     return all(sz == 1 or st == js for sz, st, js in zip(t.shape, t.stride(), jl_strides(t.shape)))
 
 

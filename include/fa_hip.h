@@ -58,7 +58,10 @@ typedef enum fa_status {
  *   l (N, 1, B) = sum_j exp(s_ij - m_i),  m (N, 1, B) = max_j s_ij,
  *   s = scale * Q K^T  (natural-log units, as src/dense.jl:78-91).
  * scale <= 0 selects the reference's tau = 1/sqrt(d) (src/dense.jl:43).
- * The reference requires Nk == N and dv == d (Appendix A.1); both are lifted. */
+ * The reference requires Nk == N and dv == d (Appendix A.1); both are lifted.
+ * Empty inputs behave as dense_fa! does with empty arrays: N == 0 or B == 0 is a
+ * no-op (no pointer is dereferenced); Nk == 0 writes O = 0, l = 0, m = -Inf, the
+ * initial state of src/dense.jl:58-60.  d, dv must be >= 1. */
 int fa_dense_fwd(int dtype,
                  const void* Q, const void* K, const void* V,
                  void* O, float* l, float* m,

@@ -62,9 +62,15 @@ def test_invalid_arguments_return_status_and_message():
     # unknown dtype
     rc = L.fa_dense_fwd(9, P, P, P, P, P, P, 4, 4, 4, 4, 1, 0.0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"dtype" in L.fa_last_error()
-    # non-positive sizes → DimensionMismatch
-    rc = L.fa_dense_fwd(1, P, P, P, P, P, P, 0, 4, 4, 4, 1, 0.0, None)
+    # negative sizes / empty head dims → DimensionMismatch
+    rc = L.fa_dense_fwd(1, P, P, P, P, P, P, -1, 4, 4, 4, 1, 0.0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"DimensionMismatch" in L.fa_last_error()
+    rc = L.fa_dense_fwd(1, P, P, P, P, P, P, 4, 4, 0, 4, 1, 0.0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"DimensionMismatch" in L.fa_last_error()
+    # empty inputs (N = 0 or batch = 0) are a no-op, as dense_fa! runs no tile
+    # (src/dense.jl:45): nothing is dereferenced or launched
+    assert L.fa_dense_fwd(1, None, None, None, None, None, None, 0, 4, 4, 4, 1, 0.0, None) == 0
+    assert L.fa_dense_fwd(1, None, None, None, None, None, None, 4, 4, 4, 4, 0, 0.0, None) == 0
     # null pointer
     rc = L.fa_dense_fwd(1, None, P, P, P, P, P, 4, 4, 4, 4, 1, 0.0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"null" in L.fa_last_error()

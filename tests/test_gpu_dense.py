@@ -299,3 +299,29 @@ def test_forced_forward_variants(fa, variant, N, Nk, d, dv, B, dtype):
     assert_close(_np(y), yr, dtype, f"y variant {variant}")
     assert_lm_close(_np(l), lr, dtype, "l")
     assert_lm_close(_np(m), mr, dtype, "m")
+
+
+def test_empty_inputs(fa):
+    """Empty arrays as dense_fa! treats them (src/dense.jl:21-102): N = 0 or batch = 0
+    runs no tile; Nk = 0 leaves the initial O = 0, l = 0, m = -Inf (:58-60).  The
+    backward's sums over an empty key or query range are 0."""
+    dev = "cuda"
+    for N, Nk, B in ((0, 10, 2), (7, 10, 0)):
+        q = fa.jl_empty((N, 64, B), torch.bfloat16, dev)
+        k = fa.jl_empty((Nk, 64, B), torch.bfloat16, dev); k.copy_(torch.randn(k.shape))
+        v = fa.jl_empty((Nk, 32, B), torch.bfloat16, dev); v.copy_(torch.randn(v.shape))
+        y, l, m = fa.dense_fa(q, k, v)
+        torch.cuda.synchronize()
+        assert tuple(y.shape) == (N, 32, B) and tuple(l.shape) == (N, 1, B)
+    q = fa.jl_empty((5, 64, 2), torch.bfloat16, dev); q.copy_(torch.randn(q.shape))
+    k = fa.jl_empty((0, 64, 2), torch.bfloat16, dev)
+    v = fa.jl_empty((0, 32, 2), torch.bfloat16, dev)
+    y, l, m = fa.dense_fa(q, k, v)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (5, 32, 2)
+    assert bool((y.float() == 0).all()) and bool((l == 0).all()) and bool(torch.isneginf(m).all())
+    dO = fa.jl_empty((5, 32, 2), torch.bfloat16, dev); dO.copy_(torch.randn(dO.shape))
+    dq, dk, dv = fa.dense_fa_backward(q, k, v, y, dO, l, m)
+    torch.cuda.synchronize()
+    assert tuple(dq.shape) == (5, 64, 2) and bool((dq.float() == 0).all())
+    assert tuple(dk.shape) == (0, 64, 2) and tuple(dv.shape) == (0, 32, 2)
