@@ -228,13 +228,14 @@ int fa_windowed_fwd(int dtype, const void* q, const void* k, const void* v, void
                     size_t workspace_bytes, void* hip_stream) {
     static const char* fn = "fa_windowed_fwd";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (d < 1 || dv < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv, batch must be >= 1");
-    if (!q || !k || !v || !y || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    if (d < 1 || dv < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv must be >= 1, batch >= 0");
     fa::WindowedArgs a{};
     const char* why = "";
     int rc = make_geom(a.g, nspatial, spatial, ws, stride, pad, &why);
     if (rc != FA_OK) return fail(rc, fn, why);
+    if (batch == 0) return ok();   // no image: windowed_fa on an empty batch computes nothing
+    if (!q || !k || !v || !y || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     a.dtype = dtype; a.q = q; a.k = k; a.v = v; a.y = y; a.l = l; a.m = m;
     a.d = d; a.dv = dv; a.batch = batch;
     a.scale = resolve_scale(scale, d);
@@ -251,12 +252,13 @@ static int window_common(const char* fn, int dtype, const void* src, void* dst, 
                          const int64_t* spatial, int64_t C, int64_t batch, int64_t ws, int64_t stride,
                          int64_t pad, bool unwindow, void* hip_stream) {
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (C < 1 || batch < 1) return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: C, batch must be >= 1");
-    if (!src || !dst) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    if (C < 1 || batch < 0) return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: C must be >= 1, batch >= 0");
     fa::WindowGeom g{};
     const char* why = "";
     int rc = make_geom(g, nspatial, spatial, ws, stride, pad, &why);
     if (rc != FA_OK) return fail(rc, fn, why);
+    if (batch == 0) return ok();   // empty batch: nothing to move
+    if (!src || !dst) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     rc = fa::launch_window(dtype, src, dst, g, C, batch, unwindow, (hipStream_t)hip_stream, &why);
     return rc == FA_OK ? ok() : fail(rc, fn, why);
 }
@@ -280,14 +282,15 @@ int fa_windowed_bwd(int dtype, const void* q, const void* k, const void* v, cons
                     void* hip_stream) {
     static const char* fn = "fa_windowed_bwd";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (d < 1 || dv < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv, batch must be >= 1");
-    if (!q || !k || !v || !y || !dy || !l || !m || !dq || !dk || !dv_)
-        return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
+    if (d < 1 || dv < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv must be >= 1, batch >= 0");
     fa::WindowedBwdArgs a{};
     const char* why = "";
     int rc = make_geom(a.g, nspatial, spatial, ws, stride, pad, &why);
     if (rc != FA_OK) return fail(rc, fn, why);
+    if (batch == 0) return ok();   // no image, no gradient element
+    if (!q || !k || !v || !y || !dy || !l || !m || !dq || !dk || !dv_)
+        return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     const size_t need = fa::windowed_workspace(dtype, a.g, d, dv, batch);
     if (need > 0 && (!workspace || workspace_bytes < need))
         return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_windowed_workspace()");
@@ -306,9 +309,10 @@ int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V, voi
                      void* hip_stream) {
     static const char* fn = "fa_circulant_fwd";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
-    if (N < 1 || d < 1 || dv < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, d, dv, batch must be >= 1");
+    if (N < 0 || d < 1 || dv < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: d, dv must be >= 1, N, batch >= 0");
     if (W < 1) return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: window size W must be >= 1");
+    if (N == 0 || batch == 0) return ok();   // circulant_fa! loops over no row / slab
     if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     fa::CircArgs a{dtype, Q, K, V, O, l, m, N, d, dv, batch, W, resolve_scale(scale, d)};
     const char* why = "";
@@ -326,8 +330,9 @@ int fa_softmax(int dtype, const void* S, void* P, int64_t M, int64_t N, int64_t 
     static const char* fn = "fa_softmax";
     if (!valid_dtype(dtype)) return fail(FA_ERR_INVALID_ARG, fn, "unknown dtype");
     if (dims != 1 && dims != 2) return fail(FA_ERR_INVALID_ARG, fn, "only softmax in dims 1 or 2 supported");
-    if (M < 1 || N < 1 || batch < 1)
-        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: M, N, batch must be >= 1");
+    if (M < 1 || N < 1 || batch < 0)
+        return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: M, N must be >= 1, batch >= 0");
+    if (batch == 0) return ok();   // no matrix to normalise
     if (!S || !P) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     const size_t need = fa::softmax_workspace(M, N, batch, dims);
     if (need > 0 && (!workspace || workspace_bytes < need))

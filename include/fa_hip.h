@@ -112,7 +112,9 @@ int fa_dense_bwd(int dtype,
  *                                  the reference, Appendix A.7)
  *   l, m: (ws^k, 1, L, B) window layout (src/windowed.jl:20-21),
  *         L = prod_i ((S_i + 2 pad - ws) / stride + 1).
- * nspatial = k in 1..3; pad < 0 selects the reference default (ws-1)/2. */
+ * nspatial = k in 1..3; pad < 0 selects the reference default (ws-1)/2.
+ * B == 0 (an empty batch) is a no-op after the geometry is validated; the
+ * same holds for fa_window, fa_unwindow and fa_windowed_bwd. */
 int fa_windowed_fwd(int dtype,
                     const void* q, const void* k, const void* v,
                     void* y, float* l, float* m,
@@ -170,7 +172,8 @@ int fa_windowed_bwd(int dtype,
  * cartesian_circulant enumerates (src/utils.jl:6-17); W > N repeats keys.
  * Q, K: (N, d, batch); V: (N, dv, batch); O: (N, dv, batch); l, m: (N, 1, batch)
  * float32 with the dense_fa! meaning.  Any W >= 1 (the reference's own
- * benchmark uses even W, bench/compare.jl:98). */
+ * benchmark uses even W, bench/compare.jl:98).  N == 0 or batch == 0 is a
+ * no-op (the reference's row and batch loops run zero times). */
 int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V,
                      void* O, float* l, float* m,
                      int64_t N, int64_t d, int64_t dv, int64_t batch, int64_t W,
@@ -183,7 +186,8 @@ int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V,
  * (M contiguous elements), dims = 2 each row S[i, :, b].  P may equal S
  * (in place, fused_softmax!(S)).  A vector is (M, 1, 1) with dims = 1.
  * Computed in fp32; an all -Inf or NaN-containing vector gives NaN, as the
- * reference's arithmetic does. */
+ * reference's arithmetic does.  batch == 0 is a no-op; M or N == 0 is
+ * rejected (a reduction over an empty dimension). */
 size_t fa_softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims);
 int fa_softmax(int dtype, const void* S, void* P, int64_t M, int64_t N, int64_t batch, int dims,
                void* workspace, size_t workspace_bytes, void* hip_stream);

@@ -71,6 +71,23 @@ def test_invalid_arguments_return_status_and_message():
     # (src/dense.jl:45): nothing is dereferenced or launched
     assert L.fa_dense_fwd(1, None, None, None, None, None, None, 0, 4, 4, 4, 1, 0.0, None) == 0
     assert L.fa_dense_fwd(1, None, None, None, None, None, None, 4, 4, 4, 4, 0, 0.0, None) == 0
+    # empty batch in the windowed / circulant / softmax entries: validated, then a
+    # no-op (the reference loops over zero images / rows / slabs)
+    sp2 = (ctypes.c_int64 * 2)(16, 16)
+    assert L.fa_windowed_fwd(1, None, None, None, None, None, None, 2, sp2, 8, 8, 0, 7, 7, 3,
+                             0.0, None, 0, None) == 0
+    assert L.fa_windowed_bwd(1, None, None, None, None, None, None, None, None, None, None, 2, sp2,
+                             8, 8, 0, 7, 7, 3, 0.0, None, 0, None) == 0
+    assert L.fa_window(1, None, None, 2, sp2, 8, 0, 7, 7, 3, None) == 0
+    assert L.fa_unwindow(1, None, None, 2, sp2, 8, 0, 7, 7, 3, None) == 0
+    rc = L.fa_windowed_fwd(1, None, None, None, None, None, None, 2, sp2, 8, 8, 0, 17, 17, 0,
+                           0.0, None, 0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"window" in L.fa_last_error()
+    assert L.fa_circulant_fwd(1, None, None, None, None, None, None, 0, 32, 32, 1, 5, 0.0, None) == 0
+    assert L.fa_circulant_fwd(1, None, None, None, None, None, None, 64, 32, 32, 0, 5, 0.0, None) == 0
+    assert L.fa_softmax(1, None, None, 8, 8, 0, 1, None, 0, None) == 0
+    rc = L.fa_softmax(1, None, None, 0, 8, 1, 1, None, 0, None)
+    assert rc == fa_hip.FA_ERR_INVALID_ARG and b"DimensionMismatch" in L.fa_last_error()
     # null pointer
     rc = L.fa_dense_fwd(1, None, P, P, P, P, P, 4, 4, 4, 4, 1, 0.0, None)
     assert rc == fa_hip.FA_ERR_INVALID_ARG and b"null" in L.fa_last_error()

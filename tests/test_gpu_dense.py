@@ -325,3 +325,32 @@ def test_empty_inputs(fa):
     torch.cuda.synchronize()
     assert tuple(dq.shape) == (5, 64, 2) and bool((dq.float() == 0).all())
     assert tuple(dk.shape) == (0, 64, 2) and tuple(dv.shape) == (0, 32, 2)
+
+
+def test_empty_batch_other_entries(fa):
+    """An empty batch through windowed_fa / its backward / window / unwindow,
+    circulant_fa (also N = 0) and fused_softmax: the reference loops over zero
+    images, rows or slabs (src/windowed.jl:3-23, src/circulant.jl:19-46,
+    src/fused_softmax.jl:1-41), so each returns correctly shaped empty outputs."""
+    dev = "cuda"
+    q = fa.jl_empty((16, 16, 8, 0), torch.bfloat16, dev)
+    y, l, m = fa.windowed_fa(q, q, q, 7)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (16, 16, 8, 0) and tuple(l.shape) == (49, 1, 9, 0)
+    dq, dk, dv = fa.windowed_fa_backward(q, q, q, y, y, l, m, 7)
+    torch.cuda.synchronize()
+    assert tuple(dq.shape) == (16, 16, 8, 0) and tuple(dv.shape) == (16, 16, 8, 0)
+    X = fa.window(q, 7)
+    assert tuple(X.shape) == (49, 8, 9, 0)
+    x = fa.unwindow(X, (16, 16, 8, 0), 7)
+    torch.cuda.synchronize()
+    assert tuple(x.shape) == (16, 16, 8, 0)
+    for N, B in ((0, 2), (64, 0)):
+        Q = fa.jl_empty((N, 32, B), torch.bfloat16, dev)
+        O, lc, mc = fa.circulant_fa(Q, Q, Q, 5)
+        torch.cuda.synchronize()
+        assert tuple(O.shape) == (N, 32, B) and tuple(lc.shape) == (N, 1, B)
+    S = fa.jl_empty((8, 8, 0), torch.float32, dev)
+    P = fa.fused_softmax(S, dims=1)
+    torch.cuda.synchronize()
+    assert tuple(P.shape) == (8, 8, 0)
