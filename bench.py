@@ -8,10 +8,31 @@ step   : one fa_dense_fwd call over this rank's (B·H) slabs of BASELINE
 FLOPs  : 4·(B·H)·N²·d per step per rank (non-causal; softmax not counted;
          SURVEY.md §8d).
 scaling: weak — every rank processes its own 64 slabs (sharding over
-         batch × head, no data-path collective; a gloo/RCCL barrier and a MAX
+         batch × head, no data-path collective; a barrier and a MAX
          all-reduce of the elapsed time are the only cross-rank calls).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--extra]
+Timing protocol:
+  1. settle: the step is launched back-to-back, untimed, until >= --settle-ms of
+     wall time has passed (default 250 ms).  From idle the GPU needs ~60 ms of
+     load to reach its sustained clock; the settle phase is DISCLOSED in the JSON
+     ("settle") together with the number measured without it ("cold": exactly W
+     warm-up steps, then the same K timed steps, measured first).
+  2. W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier
+     + torch.cuda.synchronize() on both sides; MAX over ranks.
+  3. the GPU clock and board power are sampled (amdsmi via torch.cuda) during
+     the timed region and reported ("clock").
+
+Secondary blocks on the same JSON line (never the headline `value`):
+  * "cfg5": BASELINE configs[4] = (64,16,16384,128) bf16 forward, STRONG
+    scaling: its 1024 (B·H) slabs are split over the N ranks
+    (fa_hip.shard.shard_range), each rank times its share; total TFLOP/s =
+    all ranks' FLOPs / the slowest rank's time.
+  * "cpu_baseline" (rank 0, N = 1): the reference's CPU algorithm
+    (oracle/fa_cpu.c BLAS port of dense_fa!) on configs[0] at 1 thread and at
+    the process's cores (median of 50 after 5 warm-ups), and on the whole
+    configs[1] workload (fp32).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-cfg5] [--extra]
 Multi-GPU: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
            --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 """
@@ -20,7 +41,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,54 +58,349 @@ METRIC = "effective attention TFLOP/s (fwd) at N=4096,d=64; % of bf16 MFMA peak"
 PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12   # 2516.6: 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense)
 PEAK_HBM_GBS = 8000.0
 B_, H_, N_, D_ = 4, 16, 4096, 64
+# BASELINE configs[4]: (B,H,N,d) = (64,16,16384,128), sharded over (B·H)
+CFG5_SLABS, CFG5_N, CFG5_D = 64 * 16, 16384, 128
 
 
-def _dist_init(n_gpus):
+# ----------------------------------------------------------------------------
+# process group / timing plumbing (device-agnostic: tests/test_bench_dist.py
+# drives it with gloo on CPU)
+# ----------------------------------------------------------------------------
+def dist_init(backend: str | None = None):
+    """One process per GPU; RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the
+    env (torch.distributed.run).  backend: "nccl" (= RCCL) on GPUs, "gloo"
+    for the CPU rehearsal.  Returns (dist or None, rank, world, local)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         return dist, rank, world, local
-    torch.cuda.set_device(0)
     return None, 0, 1, 0
 
 
-def _randn_jl(fa, shape, dtype, gen):
-    t = fa.jl_empty(shape, dtype)
-    t.copy_(torch.randn(tuple(shape), generator=gen, device="cuda", dtype=torch.float32))
-    return t
+def _cuda_sync():
+    torch.cuda.synchronize()
 
 
-def time_launches(fn, steps, warmup, dist=None):
-    """Barrier + sync on both sides; returns (max-over-ranks wall s, event s)."""
+def time_region(fn, steps, warmup, dist=None, sync=_cuda_sync, events=True):
+    """W untimed calls, then exactly `steps` timed calls bracketed by a barrier
+    + sync on both sides.  Returns (max-over-ranks wall s, max-over-ranks
+    device-event s of the region; == wall without events)."""
     for _ in range(warmup):
         fn()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    sync()
+    ev0 = ev1 = None
+    if events:
+        stream = torch.cuda.current_stream()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
-    ev0.record(stream)
+    if events:
+        ev0.record(stream)
     for _ in range(steps):
         fn()
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    if events:
+        ev1.record(stream)
+    sync()
     if dist is not None:
         dist.barrier()
     wall = time.perf_counter() - t0
-    ev_s = ev0.elapsed_time(ev1) / 1e3
+    ev_s = ev0.elapsed_time(ev1) / 1e3 if events else wall
     if dist is not None:
-        t = torch.tensor([wall, ev_s], device="cuda", dtype=torch.float64)
+        t = torch.tensor([wall, ev_s], dtype=torch.float64,
+                         device="cuda" if events else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, ev_s = float(t[0]), float(t[1])
     return wall, ev_s
+
+
+# kept for tools/ that import it
+def time_launches(fn, steps, warmup, dist=None):
+    return time_region(fn, steps, warmup, dist)
+
+
+def settle(fn, min_s: float, sync=_cuda_sync):
+    """Launch `fn` back-to-back (untimed) for at least min_s of wall time so the
+    GPU leaves its idle clock before anything is timed.  Returns (launches, s)."""
+    if min_s <= 0:
+        return 0, 0.0
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for _ in range(8):
+            fn()
+        n += 8
+        sync()
+        if time.perf_counter() - t0 >= min_s:
+            return n, time.perf_counter() - t0
+
+
+class ClockSampler:
+    """Samples the GPU shader clock (MHz) and board power (W) through amdsmi
+    (torch.cuda.clock_rate / power_draw) every ~1 ms on a host thread while a
+    timed region runs.  Fields are None where the box does not expose them."""
+
+    def __init__(self, device: int):
+        self.device = device
+        self.clk, self.pwr = [], []
+        self._stop = threading.Event()
+        self._th = None
+        self.ok = True
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self.clk.append(float(torch.cuda.clock_rate(self.device)))
+            except Exception:
+                self.ok = False
+                return
+            try:
+                self.pwr.append(float(torch.cuda.power_draw(self.device)))
+            except Exception:
+                pass
+            time.sleep(0.001)
+
+    def __enter__(self):
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._th is not None:
+            self._th.join(timeout=2.0)
+
+    def summary(self):
+        med = lambda xs: statistics.median(xs) if xs else None
+        pw = med(self.pwr)
+        if pw is not None and pw > 1e4:      # some amdsmi versions report microwatts
+            pw = pw / 1e6
+        return {"sclk_mhz_median": med(self.clk), "sclk_mhz_min": min(self.clk) if self.clk else None,
+                "sclk_mhz_max": max(self.clk) if self.clk else None, "samples": len(self.clk),
+                "power_w_median": pw, "source": "amdsmi (torch.cuda.clock_rate / power_draw)",
+                "peak_at_measured_clock_tflops": (256 * med(self.clk) * 1e6 * 4096 / 1e12) if self.clk else None}
+
+
+def sharded_strong(make_step, n_slabs_total: int, world: int, rank: int, dist, steps: int, warmup: int,
+                   flops_per_slab: float, sync=_cuda_sync, events=True):
+    """Strong scaling over (B·H) slabs: rank `rank` owns shard_range(n_slabs_total,
+    world, rank) (contiguous slabs, sizes differ by <= 1), builds its step with
+    make_step(n_local) and times it; no data-path collective.  Total throughput =
+    every rank's FLOPs / the slowest rank's time (MAX all-reduce)."""
+    from fa_hip.shard import shard_range
+    a, b = shard_range(n_slabs_total, world, rank)
+    n_local = b - a
+    step = make_step(n_local)
+    wall, ev_s = time_region(step, steps, warmup, dist, sync, events)
+    per = ev_s / steps
+    split = [shard_range(n_slabs_total, world, r) for r in range(world)]
+    total_flops = flops_per_slab * n_slabs_total
+    return {"slabs_total": n_slabs_total, "slab_split": [[x, y] for x, y in split],
+            "slabs_this_rank": n_local, "steps": steps, "warmup": warmup,
+            "ms_per_step_max_over_ranks": per * 1e3,
+            "tflops_total": total_flops / per / 1e12,
+            "tflops_per_gpu": total_flops / per / 1e12 / world,
+            "frac_of_peak_per_gpu": total_flops / per / 1e12 / world / PEAK_BF16_TFLOPS,
+            "scaling": "strong", "n_gpus": world}
+
+
+# ----------------------------------------------------------------------------
+# workloads
+# ----------------------------------------------------------------------------
+def _randn_jl(fa, shape, dtype, gen):
+    t = fa.jl_empty(shape, dtype)
+    t.normal_(generator=gen)
+    return t
+
+
+def cfg5_block(fa, world, rank, dist, steps, warmup):
+    """BASELINE configs[4]: dense_fa bf16 forward (N, d) = (16384, 128) over
+    1024 (B·H) slabs, split over the ranks (strong scaling)."""
+    gen = torch.Generator(device="cuda").manual_seed(4242 + rank)
+    N, d = CFG5_N, CFG5_D
+
+    def make_step(n):
+        Q, K, V = (_randn_jl(fa, (N, d, n), torch.bfloat16, gen) for _ in range(3))
+        O = fa.jl_empty((N, d, n), torch.bfloat16)
+        l = fa.jl_empty((N, 1, n))
+        m = fa.jl_empty((N, 1, n))
+        return lambda: fa.dense_fa_(O, l, m, Q, K, V)
+
+    r = sharded_strong(make_step, CFG5_SLABS, world, rank, dist, steps, warmup, 4.0 * N * N * d)
+    r["workload"] = "configs[4]: dense_fa bf16 forward, (B,H,N,d)=(64,16,16384,128), 1024 slabs split over ranks"
+    torch.cuda.empty_cache()
+    return r
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _cpu_threads():
+    """Cores this process may use: its affinity set, capped by the box's
+    OMP_NUM_THREADS share when set (the GPU box exports 16 per GPU)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline():
+    """The reference's CPU algorithm, dense_fa! (src/dense.jl:21-102), as the
+    BLAS-backed C/OpenMP port oracle/fa_cpu.c (same Br/Bc tiles, one gemm per
+    tile product, (slab x row-block) tasks), fp32:
+      * configs[0] (N,d,B·H) = (512,64,4): 1 thread and all usable cores,
+        median of 50 after 5 warm-ups (BASELINE.md 'CPU baseline plan');
+      * configs[1] (4096,64,64): the whole workload at all usable cores, median
+        of 3 after 1 warm-up -> `value` (same unit as the headline)."""
+    import numpy as np
+    from oracle import cpu_port
+    cpu_port.blas_info()
+    threads = _cpu_threads()
+    rng = np.random.default_rng(0)
+
+    def arrs(N, d, n):
+        return [np.asfortranarray(rng.standard_normal((N, d, n)).astype(np.float32)) for _ in range(3)]
+
+    def med_time(fn, reps, warm):
+        for _ in range(warm):
+            fn()
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t)
+        return statistics.median(ts)
+
+    q0, k0, v0 = arrs(512, 64, 4)
+    f0 = 4.0 * 4 * 512 * 512 * 64
+    c0 = {}
+    for th in sorted({1, threads}):
+        t = med_time(lambda: cpu_port.dense_fa_blas(q0, k0, v0, th), 50, 5)
+        c0[f"threads_{th}"] = {"ms": t * 1e3, "gflops": f0 / t / 1e9}
+    q1, k1, v1 = arrs(N_, D_, B_ * H_)
+    t1 = med_time(lambda: cpu_port.dense_fa_blas(q1, k1, v1, threads), 3, 1)
+    f1 = 4.0 * B_ * H_ * N_ * N_ * D_
+    return {"value": f1 / t1 / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "sample": f"the whole configs[1] workload (4096,64,64) fp32, BLAS-backed C/OpenMP port of dense_fa! "
+                      f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles, OpenBLAS sgemm per tile product, {threads} threads), "
+                      f"median of 3: {t1:.2f} s",
+            "configs0_fp32_512x64x4": c0,
+            "reference_published": "dense_fa Julia N=512 d=64 bs=1 Float64: 2.392 ms, unstated CPU "
+                                   "(/root/reference/logs/compare1.txt:4)"}
+
+
+def _traffic_from_profiles():
+    """HBM bytes per launch of the forward kernel from the committed rocprofv3
+    PMC summary (profiles/*fwd_traffic*.json, written by
+    profiles/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes with
+    the gfx950 FETCH_SIZE x2 correction), newest for this workload."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*fwd_traffic*.json"))):
+        try:
+            j = json.load(open(p))
+        except Exception:
+            continue
+        if j.get("workload") == "configs[1]":
+            best = j.get("hbm_bytes_per_launch")
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="untimed back-to-back launches before timing (disclosed in the JSON)")
+    ap.add_argument("--cfg5-steps", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the configs[4] strong-scaling block")
+    ap.add_argument("--extra", action="store_true", help="also time configs[2..3] (reported under 'extra')")
+    args = ap.parse_args()
+
+    dist, rank, world, local = dist_init()
+    import fa_hip
+    fa_hip.lib()
+
+    BH = B_ * H_
+    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    Q = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
+    K = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
+    V = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
+    O = fa_hip.jl_empty((N_, D_, BH), torch.bfloat16)
+    l = fa_hip.jl_empty((N_, 1, BH), torch.float32)
+    m = fa_hip.jl_empty((N_, 1, BH), torch.float32)
+    step = lambda: fa_hip.dense_fa_(O, l, m, Q, K, V)
+    flops_rank = 4.0 * BH * N_ * N_ * D_
+
+    # cold: exactly W warm-up steps from idle, then the K timed steps
+    wall_c, ev_c = time_region(step, args.steps, args.warmup, dist)
+    settle_n, settle_s = settle(step, args.settle_ms / 1e3)
+    with ClockSampler(torch.cuda.current_device()) as clk:
+        wall, ev_s = time_region(step, args.steps, args.warmup, dist)
+    value = flops_rank * world * args.steps / wall / 1e12
+    kern_s = ev_s / args.steps
+    achieved = flops_rank / kern_s / 1e12
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "TFLOP/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (torch normal_ -> bf16, column-major (N,d,B*H) device arrays)",
+        "config": {"workload": "configs[1]: dense_fa bf16 forward, (B,H,N,d)=(4,16,4096,64) per GPU",
+                   "B": B_, "H": H_, "N": N_, "d": D_, "slabs_per_gpu": BH,
+                   "global_batch_heads": BH * world, "parallelism": f"shard(B*H) x{world}, no collective"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_BF16_TFLOPS, "traffic": _traffic_from_profiles(),
+                     "kernel": "fa::dense_fwd_w8q2<bf16,64,64>",
+                     "flops_per_launch": flops_rank, "avg_launch_ms": kern_s * 1e3},
+        "settle": {"ms": settle_s * 1e3, "launches": settle_n,
+                   "why": "untimed back-to-back launches so the GPU leaves its idle clock (DESIGN.md §6)"},
+        "cold": {"value": flops_rank * world * args.steps / wall_c / 1e12,
+                 "avg_launch_ms": ev_c / args.steps * 1e3,
+                 "what": "the same K steps after exactly W warm-up steps from idle, measured before settle"},
+        "clock": clk.summary(),
+    }
+
+    if not args.no_cfg5:
+        out["cfg5"] = cfg5_block(fa_hip, world, rank, dist, args.cfg5_steps, 1)
+
+    if args.extra:
+        out["extra"] = extra_benches(fa_hip, args, dist)
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline()
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def time_graph(fn, steps, dist=None):
@@ -103,160 +421,44 @@ def time_graph(fn, steps, dist=None):
             fn()
     graph.replay()
     torch.cuda.synchronize()
-    _, e = time_launches(graph.replay, 3, 1, dist)
+    _, e = time_region(graph.replay, 3, 1, dist)
     return e / 3 / steps
-
-
-def cpu_baseline(target_s: float = 12.0):
-    """oracle/fa_cpu.c (C OpenMP port of dense_fa!, src/dense.jl:21-102, same
-    Br=64/Bc=500 tiles) on a bounded sample of the same workload: whole
-    (4096, 64) slabs in fp32, as many as fit ~target_s of CPU time."""
-    import numpy as np
-    from oracle import cpu_port
-    threads = min(16, os.cpu_count() or 1)
-    rng = np.random.default_rng(0)
-    one = lambda n: [np.asfortranarray(rng.standard_normal((N_, D_, n)).astype(np.float32)) for _ in range(3)]
-    q, k, v = one(1)
-    cpu_port.dense_fa(q, k, v, threads)              # warm-up
-    t = time.perf_counter()
-    cpu_port.dense_fa(q, k, v, threads)
-    per_slab = time.perf_counter() - t
-    n = int(max(1, min(64, target_s / max(per_slab, 1e-6))))
-    q, k, v = one(n)
-    reps, dts = max(1, min(5, int(target_s / max(per_slab * n, 1e-6)))), []
-    for _ in range(reps):                              # best of a few full passes
-        t = time.perf_counter()
-        cpu_port.dense_fa(q, k, v, threads)
-        dts.append(time.perf_counter() - t)
-    dt = min(dts)
-    flops = 4.0 * n * N_ * N_ * D_
-    return {"value": flops / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of 64 (N,d)=(4096,64) slabs of configs[1], fp32, C/OpenMP port of dense_fa! "
-                      f"(oracle/fa_cpu.c, reference tiles Br=64 Bc=500), best of {reps}: {dt:.2f} s"}
-
-
-def _traffic_from_profiles():
-    """HBM bytes per launch of the forward kernel from the committed rocprofv3
-    PMC summary (profiles/*fwd_traffic*.json, written by
-    profiles/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes with
-    the gfx950 FETCH_SIZE x2 correction), if one exists for this workload."""
-    import glob
-    best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*fwd_traffic*.json"))):
-        try:
-            j = json.load(open(p))
-        except Exception:
-            continue
-        if j.get("workload") == "configs[1]":
-            best = j.get("hbm_bytes_per_launch")
-    return best
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    # ~0.1 s of untimed launches: from idle the GPU needs ~200 launches (~60 ms)
-    # to reach its sustained clock (tools/exp/ramp.py; DESIGN.md §6)
-    ap.add_argument("--warmup", type=int, default=400)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--extra", action="store_true", help="also time configs[2..3] (reported under 'extra')")
-    args = ap.parse_args()
-
-    dist, rank, world, local = _dist_init(args.gpus)
-    import fa_hip
-    fa_hip.lib()
-
-    BH = B_ * H_
-    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
-    Q = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
-    K = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
-    V = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
-    O = fa_hip.jl_empty((N_, D_, BH), torch.bfloat16)
-    l = fa_hip.jl_empty((N_, 1, BH), torch.float32)
-    m = fa_hip.jl_empty((N_, 1, BH), torch.float32)
-    step = lambda: fa_hip.dense_fa_(O, l, m, Q, K, V)
-
-    wall, ev_s = time_launches(step, args.steps, args.warmup, dist)
-    flops_rank = 4.0 * BH * N_ * N_ * D_
-    value = flops_rank * world * args.steps / wall / 1e12
-    kern_s = ev_s / args.steps
-    achieved = flops_rank / kern_s / 1e12
-
-    out = {
-        "metric": METRIC, "value": value, "unit": "TFLOP/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic (torch.randn -> bf16, column-major (N,d,B*H) device arrays)",
-        "config": {"workload": "configs[1]: dense_fa bf16 forward, (B,H,N,d)=(4,16,4096,64) per GPU",
-                   "B": B_, "H": H_, "N": N_, "d": D_, "slabs_per_gpu": BH,
-                   "global_batch_heads": BH * world, "parallelism": f"shard(B*H) x{world}, no collective"},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_BF16_TFLOPS, "traffic": _traffic_from_profiles(),
-                     "kernel": "fa::dense_fwd_w8q2<bf16,64,64>",
-                     "flops_per_launch": flops_rank, "avg_launch_ms": kern_s * 1e3},
-    }
-
-    if args.extra:
-        out["extra"] = extra_benches(fa_hip, args, dist)
-
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline()
-    elif rank == 0:
-        out["cpu_baseline"] = None
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 def extra_benches(fa_hip, args, dist):
     """Secondary BASELINE configs (not the headline `value`)."""
     res = {}
     gen = torch.Generator(device="cuda").manual_seed(7)
-    # configs[3]: (4,16,8192,128) bf16 forward (+ backward when built)
+    # configs[3]: (4,16,8192,128) bf16 forward + backward
     N, d, BH = 8192, 128, 64
     Q, K, V = (_randn_jl(fa_hip, (N, d, BH), torch.bfloat16, gen) for _ in range(3))
     O = fa_hip.jl_empty((N, d, BH), torch.bfloat16)
     l = fa_hip.jl_empty((N, 1, BH)); m = fa_hip.jl_empty((N, 1, BH))
-    w, e = time_launches(lambda: fa_hip.dense_fa_(O, l, m, Q, K, V), max(3, args.steps // 2), 2, dist)
+    st = max(3, args.steps // 2)
+    w, e = time_region(lambda: fa_hip.dense_fa_(O, l, m, Q, K, V), st, 2, dist)
     f = 4.0 * BH * N * N * d
-    res["cfg4_fwd_tflops"] = f / (e / max(3, args.steps // 2)) / 1e12
-    try:
-        dO = _randn_jl(fa_hip, (N, d, BH), torch.bfloat16, gen)
-        steps = max(3, args.steps // 4)
-        w, e = time_launches(lambda: fa_hip.dense_fa_backward(Q, K, V, O, dO, l, m), steps, 1, dist)
-        res["cfg4_bwd_tflops"] = 2.5 * f / (e / steps) / 1e12
-        res["cfg4_fwd_bwd_tflops"] = 3.5 * f / (e / steps + f / res["cfg4_fwd_tflops"] / 1e12) / 1e12
-    except fa_hip.FlashAttentionError as ex:
-        res["cfg4_bwd"] = str(ex)
-    # configs[4]: (64,16,16384,128) over 8 GPUs -> this rank's share of 128 slabs
-    N5, d5, BH5 = 16384, 128, 128
-    Q5, K5, V5 = (_randn_jl(fa_hip, (N5, d5, BH5), torch.bfloat16, gen) for _ in range(3))
-    O5 = fa_hip.jl_empty((N5, d5, BH5), torch.bfloat16)
-    l5 = fa_hip.jl_empty((N5, 1, BH5)); m5 = fa_hip.jl_empty((N5, 1, BH5))
-    w, e = time_launches(lambda: fa_hip.dense_fa_(O5, l5, m5, Q5, K5, V5), 3, 1, dist)
-    res["cfg5_share_fwd_tflops_per_gpu"] = 4.0 * BH5 * N5 * N5 * d5 / (e / 3) / 1e12
-    del Q5, K5, V5, O5
+    res["cfg4_fwd_tflops"] = f / (e / st) / 1e12
+    dO = _randn_jl(fa_hip, (N, d, BH), torch.bfloat16, gen)
+    steps = max(3, args.steps // 4)
+    w, e = time_region(lambda: fa_hip.dense_fa_backward(Q, K, V, O, dO, l, m), steps, 1, dist)
+    res["cfg4_bwd_tflops"] = 2.5 * f / (e / steps) / 1e12
+    res["cfg4_fwd_bwd_tflops"] = 3.5 * f / (e / steps + f / res["cfg4_fwd_tflops"] / 1e12) / 1e12
+    del Q, K, V, O, dO
     # configs[2]: windowed 2-D bf16 128x128, ws=7, d=64 (B sweep)
     for Bimg in (1, 32):
-        try:
-            q, k, v = (_randn_jl(fa_hip, (128, 128, 64, Bimg), torch.bfloat16, gen) for _ in range(3))
-            t = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), args.steps, dist)
-            T, L = 49, 19 * 19
-            bytes_alg = Bimg * (3 * 128 * 128 * 64 * 2 + 128 * 128 * 64 * 2 + 2 * T * L * 4)
-            res[f"cfg3_windowed_B{Bimg}_GBs"] = bytes_alg / t / 1e9
-            res[f"cfg3_windowed_B{Bimg}_us"] = t * 1e6
-            # backward of the same shape (SURVEY §8f row 1): q, k, v, y, dy read, dq, dk, dv written
-            dy = _randn_jl(fa_hip, (128, 128, 64, Bimg), torch.bfloat16, gen)
-            y, lw, mw = fa_hip.windowed_fa(q, k, v, 7)
-            tb = time_graph(lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), max(5, args.steps // 4), dist)
-            bytes_bwd = Bimg * (8 * 128 * 128 * 64 * 2 + 2 * T * L * 4)
-            res[f"cfg3_windowed_bwd_B{Bimg}_GBs"] = bytes_bwd / tb / 1e9
-            res[f"cfg3_windowed_bwd_B{Bimg}_us"] = tb * 1e6
-        except fa_hip.FlashAttentionError as ex:
-            res[f"cfg3_windowed_B{Bimg}"] = str(ex)
+        q, k, v = (_randn_jl(fa_hip, (128, 128, 64, Bimg), torch.bfloat16, gen) for _ in range(3))
+        t = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), args.steps, dist)
+        T, L = 49, 19 * 19
+        bytes_alg = Bimg * (3 * 128 * 128 * 64 * 2 + 128 * 128 * 64 * 2 + 2 * T * L * 4)
+        res[f"cfg3_windowed_B{Bimg}_GBs"] = bytes_alg / t / 1e9
+        res[f"cfg3_windowed_B{Bimg}_us"] = t * 1e6
+        # backward of the same shape (SURVEY §8f row 1): q, k, v, y, dy read, dq, dk, dv written
+        dy = _randn_jl(fa_hip, (128, 128, 64, Bimg), torch.bfloat16, gen)
+        y, lw, mw = fa_hip.windowed_fa(q, k, v, 7)
+        tb = time_graph(lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), max(5, args.steps // 4), dist)
+        bytes_bwd = Bimg * (8 * 128 * 128 * 64 * 2 + 2 * T * L * 4)
+        res[f"cfg3_windowed_bwd_B{Bimg}_GBs"] = bytes_bwd / tb / 1e9
+        res[f"cfg3_windowed_bwd_B{Bimg}_us"] = tb * 1e6
     # circulant (SURVEY §8f row 3): the reference's runcirculant shape
     # (bench/compare.jl:105-115: N=4096, d=32, bs=1, W = 16..256) and a
     # device-scale shape (B·H=64, N=16384, d=64, W=129; HBM-bound, GB/s)
@@ -269,14 +471,13 @@ def extra_benches(fa_hip, args, dist):
         res[f"{tag}_us"] = t * 1e6
         res[f"{tag}_GBs"] = Bc * Nc * (4 * dc * 2 + 8) / t / 1e9       # Q, K, V, O + l, m
         res[f"{tag}_tflops"] = 4.0 * Bc * Nc * Wc * dc / t / 1e12
-    del Qc, Kc, Vc, Oc
     # fused softmax: a configs[1]-shaped score tensor
     # (4096 x 4096 x 64 bf16, 2 GiB) along each dim; HBM-bound: read + write
     Ssm = _randn_jl(fa_hip, (4096, 4096, 64), torch.bfloat16, gen)
     Psm = torch.empty_like(Ssm)
     for dims in (1, 2):
         steps = max(3, args.steps // 4)
-        w, e = time_launches(lambda: fa_hip.fused_softmax_(Psm, Ssm, dims), steps, 1, dist)
+        w, e = time_region(lambda: fa_hip.fused_softmax_(Psm, Ssm, dims), steps, 1, dist)
         t = e / steps
         res[f"softmax_4096x4096x64_dims{dims}_GBs"] = 2 * Ssm.numel() * 2 / t / 1e9
         res[f"softmax_4096x4096x64_dims{dims}_us"] = t * 1e6

@@ -3,7 +3,8 @@
 // Validates arguments the way the reference's Julia methods would fail
 // (DimensionMismatch → FA_ERR_INVALID_ARG), resolves the default scale
 // τ = 1/√d (src/dense.jl:43), and dispatches to the kernel launchers.  No
-// global state besides the thread-local error string; never allocates,
+// process-global state: the error string and the fa_debug_set_* knobs are
+// thread-local (the knobs are test/benchmark hooks, not ABI); never allocates,
 // synchronises or aborts.
 #include <hip/hip_runtime.h>
 
@@ -97,6 +98,15 @@ int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
 int fa_debug_set_fwd_variant(int v) {
     const int old = fa::g_fwd_variant;
     if (v == 0 || (v >= 4 && v <= 9)) fa::g_fwd_variant = v;
+    return old;
+}
+
+// Not part of the public header: lazy-rescale threshold of the bf16/f16 forward
+// kernels in log2 units (default 8; 0 = rescale on every max increase, the
+// textbook order).  Accuracy tests only; returns the previous value.
+float fa_debug_set_rescale_threshold(float t) {
+    const float old = fa::g_fwd_rescale_log2;
+    if (t >= 0.0f && t <= 16.0f) fa::g_fwd_rescale_log2 = t;
     return old;
 }
 

@@ -764,7 +764,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
     }
 }
 
-int g_bwd_force_generic = 0;   // benchmark knob
+thread_local int g_bwd_force_generic = 0;   // benchmark knob
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {

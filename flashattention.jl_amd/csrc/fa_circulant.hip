@@ -35,7 +35,7 @@
 
 namespace fa {
 
-int g_circ_force_generic = 0;   // debug knob: 1 = one-wave-per-query kernel, 2 = LDS-tiled SIMT kernel (non-MFMA shapes)
+thread_local int g_circ_force_generic = 0;   // debug knob: 1 = one-wave-per-query kernel, 2 = LDS-tiled SIMT kernel (non-MFMA shapes)
 
 struct CircParams {
     const void* Q;

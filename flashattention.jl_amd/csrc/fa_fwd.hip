@@ -48,7 +48,8 @@
 
 namespace fa {
 
-int g_fwd_variant = 0;  // 0: auto; 4..7: forced geometry (benchmark knob, fa_debug_set_fwd_variant)
+thread_local int g_fwd_variant = 0;  // 0: auto; 4..7: forced geometry (benchmark knob, fa_debug_set_fwd_variant)
+thread_local float g_fwd_rescale_log2 = kRescaleLog2;  // fa_debug_set_rescale_threshold (accuracy tests)
 
 struct FwdParams {
     const void* Q;
@@ -66,6 +67,7 @@ struct FwdParams {
     int nsplit, tps, batch;
     float *opart, *lpart, *mpart;
     float scale, scale_log2;
+    float rescale_log2;   // lazy-rescale threshold (log2 units): kRescaleLog2, or the debug knob
     int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
 };
 
@@ -552,7 +554,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
 #pragma unroll
     for (int u = 0; u < NQB; ++u) { m_used[u] = kNegInf; m_true[u] = kNegInf; l_run[u] = 0.0f; }
     const float c = p.scale_log2;
-    const float thr_raw = kRescaleLog2 / c;
+    const float thr_raw = p.rescale_log2 / c;
     const int NT = (Nk + BN - 1) / BN;
     const bool ragged = (Nk % BN) != 0;
 
@@ -855,7 +857,7 @@ __device__ __forceinline__ void dense_fwd_t16(const FwdParams& p) {
 #pragma unroll
     for (int u = 0; u < NU; ++u) { m_used[u] = kNegInf; m_true[u] = kNegInf; l_run[u] = 0.0f; }
     const float c = p.scale_log2;
-    const float thr_raw = kRescaleLog2 / c;
+    const float thr_raw = p.rescale_log2 / c;
     const int NT = (Nk + BN - 1) / BN;
     const bool ragged = (Nk % BN) != 0;
 
@@ -1163,21 +1165,31 @@ static hipError_t launch_f32(const FwdParams& p, int Dc, int DVc, dim3 grid, hip
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
-// Padded-key fast path: bf16/fp16 with Nk % 8 != 0 (or K / V not 16-B aligned)
-// copy K and V into zero-padded slabs of row stride Nk8 = roundup(Nk, 8) in the
-// caller's workspace; the fast kernels then address rows by ldk = Nk8 and mask
-// keys >= Nk as for any ragged last tile.  Without a workspace those shapes run
-// the generic kernel (fa_dense_fwd, no workspace argument).
-static bool fwd_pad_needed(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+// Padded-key fast path: bf16/fp16 K and V are copied into zero-padded slabs of
+// row stride Nk8 = roundup(Nk, 8) in the caller's workspace; the fast kernels
+// then address rows by ldk = Nk8 and mask keys >= Nk as for any ragged last
+// tile.  fa_dense_fwd_workspace reserves that copy only when the SHAPE needs it
+// (Nk % 8 != 0): the query has no pointers.  K / V that are not 16-B aligned
+// with Nk % 8 == 0 (e.g. a view at an odd element offset) take the same copy
+// when the workspace passed is large enough for it (fwd_pad_bytes_any), and the
+// generic kernel otherwise.  Without a workspace (fa_dense_fwd) those shapes run
+// the generic kernel.
+static bool fwd_pad_fits(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     const int64_t nk8 = (Nk + 7) / 8 * 8;
-    return dtype != FA_DTYPE_F32 && Nk % 8 != 0 && nk8 * d * 2 < INT32_MAX && nk8 * dv * 2 < INT32_MAX &&
+    return dtype != FA_DTYPE_F32 && nk8 * d * 2 < INT32_MAX && nk8 * dv * 2 < INT32_MAX &&
            nk8 * (d > dv ? d : dv) * batch < ((int64_t)1 << 40);
 }
-static size_t fwd_pad_bytes(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
-    if (!fwd_pad_needed(dtype, Nk, d, dv, batch)) return 0;
+static bool fwd_pad_needed(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    return Nk % 8 != 0 && fwd_pad_fits(dtype, Nk, d, dv, batch);
+}
+static size_t fwd_pad_bytes_any(int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     const int64_t nk8 = (Nk + 7) / 8 * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     return al((size_t)(nk8 * d * batch) * 2) + al((size_t)(nk8 * dv * batch) * 2) + 256;
+}
+static size_t fwd_pad_bytes(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    if (!fwd_pad_needed(dtype, Nk, d, dv, batch)) return 0;
+    return fwd_pad_bytes_any(Nk, d, dv, batch);
 }
 size_t dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     return fwd_pad_bytes(dtype, Nk, d, dv, batch) + split_plan(dtype, N, Nk, d, dv, batch).bytes;
@@ -1216,15 +1228,18 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     p.total_wg = (int)total;
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
+    p.rescale_log2 = g_fwd_rescale_log2;
     p.batch = (int)a.batch;
     p.nsplit = 1; p.tps = 0; p.opart = p.lpart = p.mpart = nullptr;
     const int epc = a.dtype == FA_DTYPE_F32 ? 4 : 8;
     p.ldk = (int)a.Nk;
-    const size_t pad_bytes = fwd_pad_bytes(a.dtype, a.Nk, a.d, a.dv, a.batch);
     p.fast = (a.Nk % epc == 0) && aligned16(a.K) && aligned16(a.V);
-    if (!p.fast && a.workspace && fwd_pad_needed(a.dtype, a.Nk, a.d, a.dv, a.batch) &&
+    // bytes of the workspace taken by the padded K / V copies (0: none made)
+    size_t pad_bytes = 0;
+    if (!p.fast && a.workspace && fwd_pad_fits(a.dtype, a.Nk, a.d, a.dv, a.batch) &&
         a.N * a.d * 2 < (int64_t)INT32_MAX &&
-        a.workspace_bytes >= pad_bytes) {
+        a.workspace_bytes >= fwd_pad_bytes_any(a.Nk, a.d, a.dv, a.batch)) {
+        pad_bytes = fwd_pad_bytes_any(a.Nk, a.d, a.dv, a.batch);
         const int64_t nk8 = (a.Nk + 7) / 8 * 8;
         char* w = (char*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
         char* kp = w;

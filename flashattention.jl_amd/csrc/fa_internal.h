@@ -109,9 +109,14 @@ inline int head_dim_class(int64_t d) {
 
 constexpr int kMaxHeadDim = 128;
 
-extern int g_fwd_variant;       // forward kernel variant (debug/benchmark knob)
-extern int g_bwd_force_generic; // backward: force the generic SIMT path (debug knob)
-extern int g_win_force_composed; // windowed: force the composed gather/dense/fold path (debug knob)
-extern int g_circ_force_generic; // circulant: force the one-wave-per-query kernel (debug knob)
+// Debug / benchmark knobs (fa_debug_set_*; not part of include/fa_hip.h and not
+// ABI state).  They are THREAD-LOCAL: a knob set on one host thread changes only
+// the kernels that thread launches, so concurrent callers on other threads stay
+// on the default paths and the public entry points remain stateless for them.
+extern thread_local int g_fwd_variant;        // forward kernel variant
+extern thread_local float g_fwd_rescale_log2; // forward fast kernels: lazy-rescale threshold (log2 units)
+extern thread_local int g_bwd_force_generic;  // backward: force the generic SIMT path
+extern thread_local int g_win_force_composed; // windowed: forced path (composed / fused variants)
+extern thread_local int g_circ_force_generic; // circulant: forced kernel
 
 }  // namespace fa

@@ -1476,7 +1476,7 @@ static bool rows_f32_ok(const WindowedArgs& a) {
            a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
 }
 
-int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default)
+thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default)
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.

@@ -136,6 +136,9 @@ def lib() -> ctypes.CDLL:
         if hasattr(L, dbg):
             getattr(L, dbg).restype = ctypes.c_int
             getattr(L, dbg).argtypes = [ctypes.c_int]
+    if hasattr(L, "fa_debug_set_rescale_threshold"):
+        L.fa_debug_set_rescale_threshold.restype = ctypes.c_float
+        L.fa_debug_set_rescale_threshold.argtypes = [ctypes.c_float]
     if L.fa_abi_version() != 1:
         raise ImportError("fa_hip: ABI version mismatch")
     _LIB = L
@@ -247,6 +250,13 @@ def dense_fa_(O: torch.Tensor, l: torch.Tensor, m: torch.Tensor,
     _device_check(Q, K, V, O, l, m)
     Lb = lib()
     nws = Lb.fa_dense_fwd_workspace(code, N, Nk, d, dv, B) if hasattr(Lb, "fa_dense_fwd_ws") else 0
+    if (code != DTYPES[torch.float32] and N * Nk * B > 0 and Nk % 8 == 0
+            and (K.data_ptr() % 16 or V.data_ptr() % 16)):
+        # K / V not 16-B aligned (a view at an odd offset): add room for the
+        # padded K / V copies the fast kernels then run on (fa_fwd.hip
+        # fwd_pad_bytes_any); the shape-only workspace query cannot see pointers
+        al = lambda x: (x + 255) & ~255
+        nws += al(Nk * d * B * 2) + al(Nk * dv * B * 2) + 256
     if nws == 0:
         _check(Lb.fa_dense_fwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(l), _ptr(m),
                                N, Nk, d, dv, B, float(scale), _stream(Q)))
@@ -361,6 +371,7 @@ def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
     _require(K.shape == (Nk, d, B) and V.shape == (Nk, dv, B), "K, V shapes disagree with Q")
     _require(O.shape == (N, dv, B) and dO.shape == (N, dv, B), "O, dO must be (N, dv, batch)")
     _require(l.shape == (N, 1, B) and m.shape == (N, 1, B), "l, m must be (N, 1, batch)")
+    _require(l.dtype == torch.float32 and m.dtype == torch.float32, "l, m must be float32")
     code = _dtype_code(Q, K, V, O, dO)
     _device_check(Q, K, V, O, dO, l, m)
     dQ = jl_empty((N, d, B), Q.dtype, Q.device)
@@ -389,13 +400,22 @@ _WS = {}
 
 
 def _workspace(device, nbytes: int) -> torch.Tensor:
-    """Scratch buffer for the C ABI's workspace arguments (cached per device,
-    grown on demand; reuse is safe because all calls run on the caller's stream
-    in order)."""
-    key = (device.type, device.index)
+    """Scratch buffer for the C ABI's workspace arguments, one per (device,
+    stream), grown on demand.
+
+    Keyed by the caller's current stream: two calls on different streams never
+    share scratch (split-KV partials, padded K / V copies, windowed / backward
+    scratch).  The buffer is allocated while that stream is current, so the
+    caching allocator ties it to that stream: when it is replaced by a larger
+    one, the old block is only handed out again to work ordered after the
+    kernels already queued on that stream (stream-ordered reuse), and calls on
+    one stream run in order, so reusing it across calls is safe."""
+    stream = torch.cuda.current_stream(device)
+    key = (device.type, device.index, stream.cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < max(int(nbytes), 1):
-        buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        with torch.cuda.stream(stream):
+            buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
         _WS[key] = buf
     return buf
 
@@ -570,10 +590,21 @@ def windowed_fa_backward(q, k, v, y, dy, l, m, windowsize: int, stride: Optional
     stride = windowsize if stride is None else int(stride)
     pad = (windowsize - 1) // 2 if pad is None else int(pad)
     D = q.dim()
+    _require(D >= 3 and all(t.dim() == D for t in (k, v, y, dy)), "q, k, v, y, dy must share rank >= 3")
     nsp = D - 2
+    _require(1 <= nsp <= 3, "1 to 3 spatial dims supported")
     sp = tuple(q.shape[:nsp])
     d, B = q.shape[D - 2], q.shape[D - 1]
     dv = v.shape[D - 2]
+    _require(tuple(k.shape) == tuple(q.shape), "k must have q's shape")
+    _require(tuple(v.shape[:nsp]) == sp and v.shape[D - 1] == B, "v must share q's spatial dims and batch")
+    _require(tuple(y.shape) == sp + (dv, B) and tuple(dy.shape) == sp + (dv, B),
+             f"y and dy must be {sp + (dv, B)}")
+    outs = window_geometry(sp, windowsize, stride, pad)
+    T, L = windowsize ** nsp, math.prod(outs)
+    _require(tuple(l.shape) == (T, 1, L, B) and tuple(m.shape) == (T, 1, L, B),
+             f"l, m must be {(T, 1, L, B)} (the forward's window statistics)")
+    _require(l.dtype == torch.float32 and m.dtype == torch.float32, "l, m must be float32")
     code = _dtype_code(q, k, v, y, dy)
     _device_check(q, k, v, y, dy, l, m)
     dq = jl_empty(sp + (d, B), q.dtype, q.device)

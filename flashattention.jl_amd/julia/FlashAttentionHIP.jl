@@ -77,6 +77,12 @@ function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
                            l::ROCArray{Float32,3}, m::ROCArray{Float32,3}) where {T}
     N, d, B = size(Q)
     Nk, dv = size(K, 1), size(V, 2)
+    size(K) == (Nk, d, B) && size(V) == (Nk, dv, B) ||
+        throw(DimensionMismatch("K, V shapes disagree with Q"))
+    size(O) == (N, dv, B) && size(dO) == (N, dv, B) ||
+        throw(DimensionMismatch("O, dO must be (N, dv, batch)"))
+    size(l) == (N, 1, B) && size(m) == (N, 1, B) ||
+        throw(DimensionMismatch("l, m must be (N, 1, batch)"))
     dQ, dK, dV = similar(Q), similar(K), similar(V)
     nws = ccall((:fa_dense_bwd_workspace, libfa_hip), Csize_t,
                 (Cint, Int64, Int64, Int64, Int64, Int64), fa_dtype(T), N, Nk, d, dv, B)
@@ -122,6 +128,14 @@ function windowed_fa_backward(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,
     nsp = N - 2
     spatial = Int64[size(q, i) for i in 1:nsp]
     d, dv, B = size(q, N - 1), size(v, N - 1), size(q, N)
+    L = prod((s + 2pad - windowsize) ÷ stride + 1 for s in spatial)
+    size(k) == size(q) || throw(DimensionMismatch("k must have q's shape"))
+    size(v)[1:nsp] == size(q)[1:nsp] && size(v, N) == B ||
+        throw(DimensionMismatch("v must share q's spatial dims and batch"))
+    size(y) == size(v) && size(dy) == size(v) ||
+        throw(DimensionMismatch("y and dy must have v's shape (spatial..., dv, batch)"))
+    size(l) == (windowsize^nsp, 1, L, B) && size(m) == (windowsize^nsp, 1, L, B) ||
+        throw(DimensionMismatch("l, m must be (ws^k, 1, L, batch), the forward's window statistics"))
     dq, dk, dv_ = similar(q), similar(k), similar(v)
     nws = ccall((:fa_windowed_workspace, libfa_hip), Csize_t,
                 (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),

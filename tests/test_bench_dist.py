@@ -1,0 +1,85 @@
+"""world_size-2 gloo rehearsal of bench.py's own multi-rank plumbing (CPU):
+process-group init from the torch.distributed.run environment, the
+configs[4] strong-scaling slab split (fa_hip.shard.shard_range), the barrier +
+MAX-over-ranks timing reduction and the JSON block — the code the driver's
+8-GPU run executes with RCCL, here with gloo and a CPU step supplied by the
+test (the product step is the HIP kernel; bench.py never computes on the CPU)."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import time
+
+import numpy as np
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      LOCAL_RANK=str(rank), WORLD_SIZE=str(world))
+    dist, r, w, _ = bench.dist_init("gloo")
+    assert (r, w) == (rank, world) and dist is not None
+    try:
+        from oracle import fa_oracle as O
+        N, d, total = 32, 8, 7
+        rng = np.random.default_rng(5)
+        q, k, v = (rng.standard_normal((N, d, total)) for _ in range(3))
+        from fa_hip.shard import shard_range
+        seen = {}
+
+        def make_step(n_local):
+            a, b = shard_range(total, w, r)
+            assert b - a == n_local
+            seen["n"] = n_local
+
+            def step():
+                y, _, _ = O.dense_fa3(q[..., a:b], k[..., a:b], v[..., a:b])
+                seen["y"] = y
+                if r == 1:
+                    time.sleep(0.05)        # the slow rank sets the reported time
+            return step
+
+        res = bench.sharded_strong(make_step, total, w, r, dist, steps=2, warmup=1,
+                                   flops_per_slab=4.0 * N * N * d, sync=lambda: None, events=False)
+        json.dumps(res)
+        a, b = shard_range(total, w, r)
+        ref, _, _ = O.dense_fa3(q, k, v)
+        out[rank] = dict(res=res, err=float(np.abs(seen["y"] - ref[..., a:b]).max()))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_bench_strong_scaling_plumbing_two_ranks():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert sorted(out.keys()) == [0, 1]
+    r0, r1 = out[0]["res"], out[1]["res"]
+    assert r0["slab_split"] == [[0, 4], [4, 7]] == r1["slab_split"]
+    assert (r0["slabs_this_rank"], r1["slabs_this_rank"]) == (4, 3)
+    # MAX over ranks: both ranks report the slow rank's time (>= its 50 ms sleep)
+    assert r0["ms_per_step_max_over_ranks"] == r1["ms_per_step_max_over_ranks"] >= 50.0
+    assert r0["tflops_total"] == r1["tflops_total"]
+    assert abs(r0["tflops_per_gpu"] * 2 - r0["tflops_total"]) < 1e-12
+    assert r0["scaling"] == "strong" and r0["n_gpus"] == 2
+    assert max(out[0]["err"], out[1]["err"]) < 1e-12
+
+
+def test_cpu_threads_respects_share(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench._cpu_threads() == min(3, len(os.sched_getaffinity(0)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench._cpu_threads() == len(os.sched_getaffinity(0))
