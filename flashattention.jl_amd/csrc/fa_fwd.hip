@@ -44,6 +44,7 @@
 
 #include "fa_common.h"
 #include "fa_internal.h"
+#include "fa_fwd_params.h"
 #include "../../include/fa_hip.h"
 
 namespace fa {
@@ -51,25 +52,7 @@ namespace fa {
 thread_local int g_fwd_variant = 0;  // 0: auto; 4..7: forced geometry (benchmark knob, fa_debug_set_fwd_variant)
 thread_local float g_fwd_rescale_log2 = kRescaleLog2;  // fa_debug_set_rescale_threshold (accuracy tests)
 
-struct FwdParams {
-    const void* Q;
-    const void* K;
-    const void* V;
-    void* O;
-    float* l;
-    float* m;
-    int N, Nk, d, dv;
-    int ldk;   // K / V row stride in elements (= Nk, or Nk rounded up to 8 in padded workspace copies)
-    int nqb, total_wg;
-    // split-KV (small grids): nsplit key ranges of tps tiles each; partial results
-    // (fp32, unnormalised, relative to the split's max) go to opart / lpart / mpart,
-    // indexed by (split * batch + b)
-    int nsplit, tps, batch;
-    float *opart, *lpart, *mpart;
-    float scale, scale_log2;
-    float rescale_log2;   // lazy-rescale threshold (log2 units): kRescaleLog2, or the debug knob
-    int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
-};
+// FwdParams: fa_fwd_params.h (shared with fa_fwd_pipe.hip)
 
 constexpr int kBM = 128;  // query rows per workgroup (4 waves x 32)
 constexpr int kBN = 64;   // keys per tile
@@ -726,6 +709,10 @@ template <class T, int D, int DV>
 __global__ __launch_bounds__(256, 2) void dense_fwd_w4q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 4, 64, 2>(p); }
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
+// occupancy variant: 32 query rows per wave, at least 4 waves per SIMD
+// (__launch_bounds__ second argument = minimum waves per SIMD: <= 128 VGPRs)
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 4) void dense_fwd_w8b64_o4(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 1>(p); }
 // split-KV instantiations of the two default geometries (small grids)
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2_split(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2, true>(p); }
@@ -1097,7 +1084,7 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         if (v == 0) v = (D <= 64 && DVc <= 64) ? 7 : 5;
         const int nw = (v == 4 || v == 6) ? 4 : 8;
         // query rows per workgroup (split kernels: 512 for w8q2 / t16q4, 256 for w8b64 / t16q2)
-        const int rows = v == 8 ? 512 : v == 9 ? 256 : 32 * nw * (v >= 6 ? 2 : 1);
+        const int rows = v == 8 ? 512 : v == 9 ? 256 : v == 16 ? 256 : 32 * nw * (v >= 6 ? 2 : 1);
         FwdParams q = p;
         q.nqb = (q.N + rows - 1) / rows;
         q.total_wg = q.nqb * (int)(p.total_wg / p.nqb) * (q.nsplit > 1 ? q.nsplit : 1);
@@ -1119,6 +1106,7 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
         else if (v == 8) { FA_LAUNCH_T(dense_fwd_t16q4) }
         else if (v == 9) { FA_LAUNCH_T(dense_fwd_t16q2) }
+        else if (v == 16) { FA_LAUNCH_T(dense_fwd_w8b64_o4) }
         else { FA_LAUNCH_T(dense_fwd_w8q2) }
 #undef FA_LAUNCH_T
         if (q.nsplit > 1) {

@@ -400,7 +400,7 @@ def test_forward_split_kv(fa, N, Nk, d, dv, B):
     assert_lm_close(_np(l1), _np(l2), "bfloat16", "l split vs unsplit")
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 16])
 @pytest.mark.parametrize("N,Nk,d,dv,B,dtype", [(300, 200, 64, 64, 2, "bfloat16"), (513, 4100, 64, 32, 1, "bfloat16"),
                                                (256, 320, 128, 128, 2, "bfloat16"), (100, 72, 32, 64, 3, "float16"),
                                                (77, 136, 128, 64, 1, "float16"), (1024, 1024, 96, 96, 1, "bfloat16")])
