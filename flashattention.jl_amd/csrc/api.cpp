@@ -117,6 +117,15 @@ int fa_debug_set_bwd_generic(int v) {
     return old;
 }
 
+// Not part of the public header: backward MFMA path (0 auto, 1 the dK/dV + dQ
+// passes, 2 the single pass wherever its shape conditions hold, 3 as 2 with the
+// hand-off's timeout word preset, which exercises the dQ fallback pass).
+int fa_debug_set_bwd_mode(int v) {
+    const int old = fa::g_bwd_mode;
+    fa::g_bwd_mode = (v >= 1 && v <= 3) ? v : 0;
+    return old;
+}
+
 // Not part of the public header: circulant kernel override (1 one-wave-per-query,
 // 2 LDS-tiled SIMT; 0 auto).
 int fa_debug_set_circ_generic(int v) {

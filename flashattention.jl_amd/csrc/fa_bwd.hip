@@ -35,6 +35,12 @@ struct BwdParams {
     int N, Nk, d, dv, batch;
     int nblk, total_wg;          // fast path: row blocks per slab, workgroups
     float scale, scale_log2;
+    // single-pass kernel (bwd_fused): dQ hand-off state, all in the caller's workspace
+    unsigned* flags = nullptr;   // [batch][nqt] members that have published slice t (zeroed per call)
+    unsigned* err = nullptr;     // hand-off timeout flag (zeroed per call)
+    float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
+    int nkb = 0, nqt = 0, hoff = 2, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
+    const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
 };
 
 template <class T> __device__ __forceinline__ float to_f(T x) { return (float)x; }
@@ -488,6 +494,16 @@ __device__ __forceinline__ void dma_image(__amdgpu_buffer_rsrc_t rs, char* img, 
     }
 }
 
+// Inter-workgroup words of the single-pass kernel: global (never flat), agent
+// scope, relaxed (global_load / global_store ... sc1).
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ unsigned ld_agent(gu32* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(gu32* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Per-lane constant parts of the two fragment reads of an image.
 struct FragAddr {
     int tr[2][2];   // [token block tb][s & 1] byte offset of the transposed read (half2 = 0)
@@ -500,6 +516,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_fast(BwdParams p) {
     typedef typename Frag8<T>::half F4;
     constexpr int KB = D * 128, VB = DV * 128, STAGE = KB + VB;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    // fallback after bwd_fused: recompute dQ only if its hand-off timed out
+    if (p.guard && ld_agent((gu32*)(uintptr_t)p.guard) == 0u) return;
     const int lid = xcd_remap(blockIdx.x, p.total_wg);
     const int b = lid / p.nblk, qb = lid - b * p.nblk;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -764,16 +782,326 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
     }
 }
 
+// --------------------------------------------------------------------------
+// Single-pass backward: the five MFMA products of OneDFastBack
+// (src_cpp/FlashAttention.cpp:221-251) — S, dP, dVᵀ += dOᵀP, dKᵀ += QᵀdS and
+// dQᵀ += KᵀdSᵀ — in one sweep, instead of the dK/dV pass plus a dQ pass that
+// recomputes S and dP (7 products).
+//
+// A workgroup = 8 waves = 256 keys of one slab (member j of the slab's K = Nk/256
+// workgroups); wave w keeps dKᵀ, dVᵀ of its 32 keys in registers (the dK/dV pass's
+// layout) and the workgroup sweeps the slab's 64-query slices.  Per slice, dS goes
+// through LDS once as a [key][query] image, and wave w computes one 32 x 32 tile of
+// dQᵀ over all 256 keys from it and the K image.  The slab's K workgroups sum each
+// slice's dQ in a FIXED order (deterministic, no atomics): member j sweeps the
+// slices rotated by 2j (step i: slice (i − 2j) mod T), so the member that adds to a
+// slice after member j does so two steps later; the running fp32 sum is handed over
+// through the workspace with sc1 stores, a per-slice counter (one lane, sc1) that the
+// next member polls (one lane) before a barrier, and sc1 loads
+// (MI355X_MICROARCH § visibility, first row of the sc1 hand-off table; 1 WG per CU).
+// Every member of a slab must be resident at once: dispatch order within an XCD
+// is monotone, so a slab's members are dealt either to one XCD (K <= 32) or across
+// all of them; each poll is bounded (~20 ms of s_memrealtime), and a timeout sets
+// `err`, which lets the guarded bwd_dq_fast that follows recompute dQ (dK, dV do
+// not depend on the hand-off).
+// --------------------------------------------------------------------------
+__device__ __forceinline__ int sig32(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+// [R rows][64 tokens] LDS image written by 8 waves (cf. dma_image).
+template <int R>
+__device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img, int ntok, int t0, int wave, int lane) {
+    constexpr int NB = R / 8;                          // 1-KiB blocks
+#pragma unroll
+    for (int it = 0; it < (NB + 7) / 8; ++it) {
+        const int blk = it * 8 + wave;
+        if (NB % 8 == 0 || blk < NB) {
+            const int P = blk * 64 + lane;
+            const int f = P >> 3, c = (P & 7) ^ swz16(f);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16,
+                (f * ntok + t0 + 8 * c) * 2, 0, 0, 0);
+        }
+    }
+}
+
+constexpr uint64_t kSpinTicks = 2000000;   // s_memrealtime (100 MHz): 20 ms
+
+// One lane waits until *f >= want; false after a timeout (then *err = 1).
+__device__ __noinline__ void wait_count(gu32* f, unsigned want, gu32* err) {
+    if (ld_agent(f) >= want) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (ld_agent(f) >= want || ld_agent(err) != 0u) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+            st_agent(err, 1u);
+            return;
+        }
+    }
+}
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    constexpr int KSUB = D * 128;                  // K image of 64 keys: [D][64]
+    constexpr int QB = D * 128, OB = DV * 128;
+    constexpr int STAGE = QB + OB + 512;           // Q, dO images + (−lse, −D) of one slice
+    constexpr int DSB = 256 * 128;                 // dSᵀ image [256 keys][64 queries]
+    constexpr int NTQ = D / 16;                    // 32 x 32 dQᵀ tiles per slice (<= 8 waves)
+    __shared__ __attribute__((aligned(16))) char smem[4 * KSUB + STAGE + DSB];
+    char* const kimg = smem;
+    char* const qimg = smem + 4 * KSUB;
+    char* const oimg = qimg + QB;
+    float* const rowc = (float*)(oimg + OB);       // −lse[64] (raw units), −D[64]
+    char* const dsimg = qimg + STAGE;
+
+    const int lid = p.xcd ? xcd_remap(blockIdx.x, p.total_wg) : (int)blockIdx.x;
+    const int KM = p.nkb, NS = p.nqt, OFF = p.hoff;   // members per slab, slices
+    const int b = lid / KM, j = lid - b * KM;
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int N = p.N, Nk = p.Nk;
+    const auto qrs = bslab<T>(p.Q, (int64_t)b * N * D, (int64_t)N * D);
+    const auto ors = bslab<T>(p.dO, (int64_t)b * N * DV, (int64_t)N * DV);
+    const auto krs = bslab<T>(p.K, (int64_t)b * Nk * D, (int64_t)Nk * D);
+    const auto vrs = bslab<T>(p.V, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
+    const int key0 = j * 256;
+    const int kj = key0 + 32 * wave + sig32(r);   // this lane's key (column of S, dP, dKᵀ, dVᵀ)
+    const bool key_ok = kj < Nk;
+    const float c = p.scale_log2;
+    const float* nlse = p.nlse + (int64_t)b * N;
+    const float* nDg = p.nD + (int64_t)b * N;
+    const int64_t pslab = (int64_t)NS * NTQ * 1024;   // floats of running sums per slab
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.part + b * pslab), (short)0, (int)(pslab * 4),
+                                                       0x00020000);
+    gu32* const flg = (gu32*)(p.flags + (int64_t)b * NS);
+    gu32* const err = (gu32*)p.err;
+
+    const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    int tro[2][2];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+            const int sw = ((sp << 1) | h) | (((qq >> 1) & 1) << 2);
+            tro[tb][sp] = (8 * h + qq) * 128 + (((tb * 4 + kh * 2 + (sig >> 1)) ^ sw) * 16) + (sig & 1) * 8;
+        }
+    const int rsw = swz16(r);
+    auto trfrag = [&](const char* img, int tb, int s) -> F8 {
+        const char* a = img + tro[tb][s & 1] + 16 * s * 128;
+        const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+        const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto rowfrag = [&](const char* img, int cb, int tb, int s2) -> F8 {
+        return *(const F8*)(img + (cb * 32 + r) * 128 + (((tb * 4 + 2 * s2 + h) ^ rsw) * 16));
+    };
+    auto slice_of = [&](int i) {
+        int t = (i - OFF * j) % NS;
+        return t < 0 ? t + NS : t;
+    };
+    // chain position of this member for slice t: the members that reach t first
+    // (steps (t + OFF·j') mod NS ascending) are j' >= ceil((NS − t)/OFF), then 0, 1, ...
+    auto chain_pos = [&](int t) {
+        const int w0 = (NS - t + OFF - 1) / OFF;
+        const int head = w0 < KM ? w0 : 0;
+        const int pos = j - head;
+        return pos < 0 ? pos + KM : pos;
+    };
+    auto load_rowc = [&](int t) {
+        const int q = t * 64 + (tid & 63);
+        float v = 0.0f;
+        if (tid < 64) v = q < N ? nlse[q] : kNegInf;
+        else if (tid < 128) v = q < N ? nDg[q] : 0.0f;
+        return v;
+    };
+
+    // ---- prologue: K images (once), the first slice, V fragments of this lane's key ----
+    int t = slice_of(0);
+    {
+        const float rc = load_rowc(t);
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) dma_image8<D>(krs, kimg + i4 * KSUB, Nk, key0 + 64 * i4, wave, lane);
+        dma_image8<D>(qrs, qimg, N, t * 64, wave, lane);
+        dma_image8<DV>(ors, oimg, N, t * 64, wave, lane);
+        if (tid < 128) rowc[tid] = rc;
+    }
+    F8 vf[DV / 16];
+#pragma unroll
+    for (int s = 0; s < DV / 16; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const T x = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(vrs, ((16 * s + 8 * h + e) * Nk + kj) * 2, 0, 0));
+            vf[s][e] = key_ok ? x : (T)0.0f;
+        }
+    f32x16 dk[D / 32], dv[DV / 32];
+#pragma unroll
+    for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) dk[cb][x] = 0.0f;
+#pragma unroll
+    for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) dv[cb][x] = 0.0f;
+    const char* const kmine = kimg + (wave >> 1) * KSUB;   // the 64-key image holding this wave's keys
+    const int ktb = wave & 1;
+    const int dsrow = 32 * wave + sig32(r);                  // this lane's dSᵀ row
+    const int cbq = wave % (D / 32), uq = wave / (D / 32);   // this wave's dQᵀ tile (wave < NTQ)
+
+    int t_prev = 0, pos_prev = 0;
+    bool pub_prev = false;
+    for (int i = 0; i < NS; ++i) {
+        t = slice_of(i);
+        const int pos = chain_pos(t);
+        const bool tail = pos == KM - 1;
+        // B1: this slice's images landed, last step's sums drained; one lane has
+        // seen the predecessor's count for slice t (the barrier releases the rest)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (pos > 0 && tid == 0) wait_count(flg + t, (unsigned)pos, err);
+        __syncthreads();
+        if (pub_prev && tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
+
+        // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x16 sa, dp;
+            const f32x4* Lq = (const f32x4*)(rowc + u * 32 + 8 * h);
+            const f32x4* Dq = (const f32x4*)(rowc + 64 + u * 32 + 8 * h);
+            const f32x4 l0 = Lq[0], l1 = Lq[1], l2 = Lq[4], l3 = Lq[5];
+            const f32x4 d0 = Dq[0], d1 = Dq[1], d2 = Dq[4], d3 = Dq[5];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sa[e] = l0[e]; sa[4 + e] = l1[e]; sa[8 + e] = l2[e]; sa[12 + e] = l3[e];
+                dp[e] = d0[e]; dp[4 + e] = d1[e]; dp[8 + e] = d2[e]; dp[12 + e] = d3[e];
+            }
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) sa = mfma32x32x16(trfrag(qimg, u, s), trfrag(kmine, ktb, s), sa);
+#pragma unroll
+            for (int s = 0; s < DV / 16; ++s) dp = mfma32x32x16(trfrag(oimg, u, s), vf[s], dp);
+            F8 pf[2], dsf[2];
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = key_ok ? exp2_fast(sa[x] * c) : 0.0f;
+                pf[x >> 3][x & 7] = (T)pr;
+                dsf[x >> 3][x & 7] = (T)(pr * dp[x]);
+            }
+#pragma unroll
+            for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) dv[cb] = mfma32x32x16(rowfrag(oimg, cb, u, s2), pf[s2], dv[cb]);
+#pragma unroll
+            for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) dk[cb] = mfma32x32x16(rowfrag(qimg, cb, u, s2), dsf[s2], dk[cb]);
+            // dSᵀ row kj: queries 32u + 16 s2 + 8h + {0..7}
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swz16(dsrow)) * 16)) = dsf[s2];
+        }
+
+        // running sum of the members before this one (sc1 loads, after B1)
+        const bool has_tile = wave < NTQ;
+        const int pofs = (t * NTQ + wave) * 4096 + lane * 16;
+        u32x4 pin[4];
+        if (pos > 0 && has_tile) {
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) pin[c4] = __builtin_amdgcn_raw_buffer_load_b128(prs, pofs + c4 * 1024, 0, 16);
+        }
+        __syncthreads();   // B2: dSᵀ complete, the slice's images free
+
+        // next slice's images and row constants (land before the next B1)
+        float rc = 0.0f;
+        if (i + 1 < NS) {
+            const int tn = slice_of(i + 1);
+            rc = load_rowc(tn);
+            dma_image8<D>(qrs, qimg, N, tn * 64, wave, lane);
+            dma_image8<DV>(ors, oimg, N, tn * 64, wave, lane);
+        }
+
+        // ---- dQᵀ tile (features 32 cbq.., queries 32 uq..) over the 256 keys ----
+        if (has_tile) {
+            f32x16 acc;
+#pragma unroll
+            for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk)
+                acc = mfma32x32x16(rowfrag(kimg + (kk >> 2) * KSUB, cbq, (kk >> 1) & 1, kk & 1), trfrag(dsimg, uq, kk), acc);
+            if (pos > 0) {
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pin[c4][e]);
+            }
+            if (tail) {
+                // 32-bit lane offset + scalar row offset (no hoisted 64-bit addresses)
+                const int q = t * 64 + 32 * uq + sig32(r);
+                const auto qo = bslab<T>(p.dQ, (int64_t)b * N * D, (int64_t)N * D);
+                const int vo = ((cbq * 32 + 4 * h) * N + q) * 2;
+                if (q < N) {
+#pragma unroll
+                    for (int x = 0; x < 16; ++x)
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[x] * p.scale)), qo,
+                                                              vo, ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
+                }
+            } else {
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
+                                      __float_as_uint(acc[4 * c4 + 2]), __float_as_uint(acc[4 * c4 + 3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);
+                }
+            }
+        }
+        if (i + 1 < NS && tid < 128) rowc[tid] = rc;
+        t_prev = t;
+        pos_prev = pos;
+        pub_prev = !tail;
+    }
+    if (pub_prev) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
+    }
+    if (key_ok) {
+        const auto ko = bslab<T>(p.dK, (int64_t)b * Nk * D, (int64_t)Nk * D);
+        const auto vo = bslab<T>(p.dV, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
+        const int lo = (4 * h * Nk + kj) * 2;
+#pragma unroll
+        for (int cb = 0; cb < D / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(dk[cb][x] * p.scale)), ko, lo,
+                                                      (cb * 32 + (x & 3) + 8 * (x >> 2)) * Nk * 2, 0);
+#pragma unroll
+        for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)dv[cb][x]), vo, lo,
+                                                      (cb * 32 + (x & 3) + 8 * (x >> 2)) * Nk * 2, 0);
+    }
+}
+
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
+thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
+    const bool fused = p.part != nullptr;
+    if (fused) {   // single pass; dQ pass below only after a hand-off timeout
+        p.total_wg = p.nkb * p.batch;
+        hipLaunchKernelGGL((bwd_fused<T, D, DV>), dim3((unsigned)p.total_wg), dim3(512), 0, s, p);
+        p.guard = p.err;
+    }
     p.nblk = (p.N + 127) / 128;
     p.total_wg = p.nblk * p.batch;
     hipLaunchKernelGGL((bwd_dq_fast<T, D, DV>), dim3((unsigned)p.total_wg), dim3(256), 0, s, p);
-    p.nblk = (p.Nk + 127) / 128;
-    p.total_wg = p.nblk * p.batch;
-    hipLaunchKernelGGL((bwd_dkdv_fast<T, D, DV>), dim3((unsigned)p.total_wg), dim3(256), 0, s, p);
+    if (!fused) {
+        p.nblk = (p.Nk + 127) / 128;
+        p.total_wg = p.nblk * p.batch;
+        hipLaunchKernelGGL((bwd_dkdv_fast<T, D, DV>), dim3((unsigned)p.total_wg), dim3(256), 0, s, p);
+    }
     return hipGetLastError();
 }
 template <class T, int D>
@@ -835,10 +1163,45 @@ static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, 
     return pl;
 }
 
+// Single-pass plan (bwd_fused) on the shape the fast kernels run (padded or not):
+// K = ceil(Nk/256) members per slab, T = ceil(N/64) slices, step offset 2 (needs
+// 2K <= T); every member of a slab resident at once (K <= CUs; one XCD per slab
+// when K <= CUs/8 and the slab count is a multiple of 8); auto only when the grid
+// fills the chip once.  Workspace: per-slice counters + timeout word, then the
+// running fp32 dQ sums (4·N·d bytes per slab).
+struct FusedPlan {
+    bool on = false;
+    int nkb = 0, nqt = 0, xcd = 0;
+    size_t flag_bytes = 0, bytes = 0;
+};
+static int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return cus;
+}
+static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    FusedPlan f;
+    if (dtype == FA_DTYPE_F32 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
+    const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
+    const int cus = device_cus();
+    if (cus < 8 || 2 * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
+    if (g_bwd_mode < 2 && batch * K < cus) return f;
+    f.on = true;
+    f.nkb = (int)K;
+    f.nqt = (int)T;
+    f.xcd = (K <= cus / 8 && batch % 8 == 0) ? 1 : 0;
+    f.flag_bytes = al256((size_t)(batch * T) * 4) + 256;
+    f.bytes = f.flag_bytes + al256((size_t)(batch * T * (d / 16)) * 4096) + 256;
+    return f;
+}
+
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     const BwdPad pl = pad_plan(dtype, N, Nk, d, dv, batch);
     const int64_t rows = pl.on ? pl.Np : N;
-    return (size_t)(2 * rows * batch * sizeof(float) + 256) + (pl.on ? pl.bytes + 256 : 0);
+    const FusedPlan fz = pl.on ? fused_plan(dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp, batch)
+                               : fused_plan(dtype, N, Nk, d, dv, batch);
+    return (size_t)(2 * rows * batch * sizeof(float) + 256) + (pl.on ? pl.bytes + 256 : 0) + fz.bytes;
 }
 
 // dst (Np, Cp, B) <- src (N, C, B), zero-filled
@@ -970,6 +1333,20 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             *why = "workspace smaller than fa_dense_bwd_workspace()";
             return FA_ERR_WORKSPACE;
         }
+        const FusedPlan fz = fused_plan(a.dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp, B);
+        if (fz.on && (size_t)(w - (char*)a.workspace) + fz.bytes <= a.workspace_bytes) {
+            p.flags = (unsigned*)w;
+            p.err = (unsigned*)(w + fz.flag_bytes - 256);
+            p.part = (float*)(w + fz.flag_bytes);
+            p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
+            // mode 3 (tests): the timeout word starts set, so every poll gives up
+            // and the guarded dQ pass must recompute dQ
+            if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
+                (g_bwd_mode == 3 && (e = hipMemsetAsync(p.err, 1, 4, s)) != hipSuccess)) {
+                *why = hipGetErrorString(e);
+                return FA_ERR_HIP;
+            }
+        }
         const bool half = a.dtype == FA_DTYPE_F16;
         auto pad = [&](const void* src, void* dst, int64_t N, int64_t C, int64_t Np, int64_t Cp) {
             return half ? pad_launch<f16>(src, dst, N, C, Np, Cp, B, s) : pad_launch<bf16>(src, dst, N, C, Np, Cp, B, s);
@@ -1002,6 +1379,23 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             return FA_ERR_HIP;
         }
         return FA_OK;
+    }
+    if (fast) {
+        const FusedPlan fz = fused_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
+        char* w = (char*)ws + al256((size_t)(2 * a.N * a.batch) * sizeof(float));
+        if (fz.on && (size_t)(w - (char*)a.workspace) + fz.bytes <= a.workspace_bytes) {
+            p.flags = (unsigned*)w;
+            p.err = (unsigned*)(w + fz.flag_bytes - 256);
+            p.part = (float*)(w + fz.flag_bytes);
+            p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
+            // mode 3 (tests): the timeout word starts set, so every poll gives up
+            // and the guarded dQ pass must recompute dQ
+            if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
+                (g_bwd_mode == 3 && (e = hipMemsetAsync(p.err, 1, 4, s)) != hipSuccess)) {
+                *why = hipGetErrorString(e);
+                return FA_ERR_HIP;
+            }
+        }
     }
     switch (a.dtype) {
         case FA_DTYPE_BF16: e = launch_typed<bf16>(p, s, fast); break;

@@ -132,7 +132,7 @@ def lib() -> ctypes.CDLL:
     L.fa_softmax.argtypes = [ctypes.c_int, vp, vp, i64, i64, i64, ctypes.c_int, vp, ctypes.c_size_t, vp]
     del fp
     for dbg in ("fa_debug_set_fwd_variant", "fa_debug_set_bwd_generic", "fa_debug_set_win_composed",
-                "fa_debug_set_circ_generic"):
+                "fa_debug_set_circ_generic", "fa_debug_set_bwd_mode"):
         if hasattr(L, dbg):
             getattr(L, dbg).restype = ctypes.c_int
             getattr(L, dbg).argtypes = [ctypes.c_int]

@@ -207,3 +207,52 @@ def test_backward_f32_mfma_path(fa, N, Nk, d, dv):
     for a, g_, r_, nm in zip(mf, gen, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
         assert_grad_close(_np(a), r_, "float32", nm)
         assert_grad_close(_np(a), _np(g_), "float32", nm + " vs generic")
+
+
+def _bwd_mode(fa, mode, *args):
+    L = fa.lib()
+    old = L.fa_debug_set_bwd_mode(mode)
+    try:
+        out = fa.dense_fa_backward(*args)
+        torch.cuda.synchronize()
+    finally:
+        L.fa_debug_set_bwd_mode(old)
+    return out
+
+
+@pytest.mark.parametrize("N,Nk,d,dv,B", [(512, 512, 64, 64, 2), (1024, 1024, 128, 128, 2), (1000, 520, 128, 64, 3),
+                                         (256, 256, 32, 32, 4), (2048, 1024, 64, 128, 1), (513, 300, 40, 24, 2),
+                                         (4096, 2048, 128, 128, 1)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_backward_single_pass(fa, N, Nk, d, dv, B, dtype):
+    """The single-pass kernel (five MFMA products, dQ summed across the slab's
+    key-block workgroups by the ordered hand-off) forced on small grids: against
+    the float64 oracle and the split dK/dV + dQ passes, and bitwise reproducible."""
+    tdt = torch.bfloat16 if dtype == "bfloat16" else torch.float16
+    rng = np.random.default_rng(N * 7 + Nk + d + dv)
+    cast = lambda a: torch.tensor(a).to(tdt).double().numpy()
+    q, k = cast(rng.standard_normal((N, d, B))), cast(rng.standard_normal((Nk, d, B)))
+    v, do = cast(rng.standard_normal((Nk, dv, B))), cast(rng.standard_normal((N, dv, B)))
+    Q, K, V, dO = (fa.jl_tensor(a, tdt) for a in (q, k, v, do))
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    one = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m)
+    again = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m)
+    split = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m)
+    dqr, dkr, dvr = O.dense_fa_backward(q, k, v, _np(Oo), do, _np(l), _np(m))
+    for a, a2, sp, r_, nm in zip(one, again, split, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+        assert torch.equal(a, a2), nm + " not reproducible"
+        assert_grad_close(_np(a), r_, dtype, nm)
+        assert_grad_close(_np(a), _np(sp), dtype, nm + " vs split passes")
+
+
+def test_backward_single_pass_fallback(fa):
+    """A hand-off timeout (forced: the timeout word starts set) leaves dK, dV of the
+    single pass and recomputes dQ in the guarded dQ pass: the result still matches."""
+    rng = np.random.default_rng(17)
+    N, d, B = 1024, 128, 2
+    Q, K, V, dO = (fa.jl_tensor(rng.standard_normal((N, d, B)), torch.bfloat16) for _ in range(4))
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    fb = _bwd_mode(fa, 3, Q, K, V, Oo, dO, l, m)
+    sp = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m)
+    for a, b_, nm in zip(fb, sp, ("dQ", "dK", "dV")):
+        assert_grad_close(_np(a), _np(b_), "bfloat16", nm + " (fallback) vs split passes")
