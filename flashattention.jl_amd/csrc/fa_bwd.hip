@@ -39,7 +39,8 @@ struct BwdParams {
     unsigned* flags = nullptr;   // [batch][nqt] members that have published slice t (zeroed per call)
     unsigned* err = nullptr;     // hand-off timeout flag (zeroed per call)
     float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
-    int nkb = 0, nqt = 0, hoff = 2, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
+    int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
+    int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
 };
 
@@ -794,8 +795,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // through LDS once as a [key][query] image, and wave w computes one 32 x 32 tile of
 // dQᵀ over all 256 keys from it and the K image.  The slab's K workgroups sum each
 // slice's dQ in a FIXED order (deterministic, no atomics): member j sweeps the
-// slices rotated by 2j (step i: slice (i − 2j) mod T), so the member that adds to a
-// slice after member j does so two steps later; the running fp32 sum is handed over
+// slices rotated by 3j (step i: slice (i − 3j) mod T), so the member that adds to a
+// slice after member j does so three steps later; the running fp32 sum is handed over
 // through the workspace with sc1 stores, a per-slice counter (one lane, sc1) that the
 // next member polls (one lane) before a barrier, and sc1 loads
 // (MI355X_MICROARCH § visibility, first row of the sc1 hand-off table; 1 WG per CU).
@@ -959,11 +960,15 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // B1: this slice's images landed, last step's sums drained; one lane has
         // seen the predecessor's count for slice t (the barrier releases the rest)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (pos > 0 && tid == 0) wait_count(flg + t, (unsigned)pos, err);
+        if (pos > 0 && tid == 0 && !(p.ablate & 1)) wait_count(flg + t, (unsigned)pos, err);
         __syncthreads();
         if (pub_prev && tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
+        const bool has_tile = wave < NTQ;
+        const int pofs = (t * NTQ + wave) * 4096 + lane * 16;
+        const bool ldpin = pos > 0 && has_tile && !(p.ablate & 10);
+        u32x4 pin[4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             f32x16 sa, dp;
@@ -1001,11 +1006,9 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swz16(dsrow)) * 16)) = dsf[s2];
         }
 
-        // running sum of the members before this one (sc1 loads, after B1)
-        const bool has_tile = wave < NTQ;
-        const int pofs = (t * NTQ + wave) * 4096 + lane * 16;
-        u32x4 pin[4];
-        if (pos > 0 && has_tile) {
+        // running sum of the members before this one (sc1 loads, after B1; issuing
+        // them halfway through this phase instead measured the same)
+        if (ldpin) {
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) pin[c4] = __builtin_amdgcn_raw_buffer_load_b128(prs, pofs + c4 * 1024, 0, 16);
         }
@@ -1028,7 +1031,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk)
                 acc = mfma32x32x16(rowfrag(kimg + (kk >> 2) * KSUB, cbq, (kk >> 1) & 1, kk & 1), trfrag(dsimg, uq, kk), acc);
-            if (pos > 0) {
+            if (ldpin) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4)
 #pragma unroll
@@ -1038,19 +1041,17 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 // 32-bit lane offset + scalar row offset (no hoisted 64-bit addresses)
                 const int q = t * 64 + 32 * uq + sig32(r);
                 const auto qo = bslab<T>(p.dQ, (int64_t)b * N * D, (int64_t)N * D);
-                const int vo = ((cbq * 32 + 4 * h) * N + q) * 2;
-                if (q < N) {
+                const int vo = q < N ? ((cbq * 32 + 4 * h) * N + q) * 2 : N * D * 2;   // past N: dropped
 #pragma unroll
-                    for (int x = 0; x < 16; ++x)
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[x] * p.scale)), qo,
-                                                              vo, ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
-                }
-            } else {
+                for (int x = 0; x < 16; ++x)
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[x] * p.scale)), qo, vo,
+                                                          ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
+            } else if (!(p.ablate & 18)) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4) {
                     const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
                                       __float_as_uint(acc[4 * c4 + 2]), __float_as_uint(acc[4 * c4 + 3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);   // sc1
                 }
             }
         }
@@ -1164,8 +1165,8 @@ static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, 
 }
 
 // Single-pass plan (bwd_fused) on the shape the fast kernels run (padded or not):
-// K = ceil(Nk/256) members per slab, T = ceil(N/64) slices, step offset 2 (needs
-// 2K <= T); every member of a slab resident at once (K <= CUs; one XCD per slab
+// K = ceil(Nk/256) members per slab, T = ceil(N/64) slices, step offset 3 (needs
+// 3K <= T); every member of a slab resident at once (K <= CUs; one XCD per slab
 // when K <= CUs/8 and the slab count is a multiple of 8); auto only when the grid
 // fills the chip once.  Workspace: per-slice counters + timeout word, then the
 // running fp32 dQ sums (4·N·d bytes per slab).
@@ -1185,8 +1186,8 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     if (dtype == FA_DTYPE_F32 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
     const int cus = device_cus();
-    if (cus < 8 || 2 * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
-    if (g_bwd_mode < 2 && batch * K < cus) return f;
+    if (cus < 8 || 3 * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
+    if ((g_bwd_mode == 0 || g_bwd_mode == 1) && batch * K < cus) return f;
     f.on = true;
     f.nkb = (int)K;
     f.nqt = (int)T;
@@ -1339,6 +1340,7 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             p.err = (unsigned*)(w + fz.flag_bytes - 256);
             p.part = (float*)(w + fz.flag_bytes);
             p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
+            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
             // mode 3 (tests): the timeout word starts set, so every poll gives up
             // and the guarded dQ pass must recompute dQ
             if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
@@ -1388,6 +1390,7 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             p.err = (unsigned*)(w + fz.flag_bytes - 256);
             p.part = (float*)(w + fz.flag_bytes);
             p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
+            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
             // mode 3 (tests): the timeout word starts set, so every poll gives up
             // and the guarded dQ pass must recompute dQ
             if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
