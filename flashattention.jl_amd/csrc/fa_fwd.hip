@@ -450,7 +450,7 @@ __global__ __launch_bounds__(kThreads) void dense_fwd_generic_f32(FwdParams p) {
 // barrier per tile, lazy rescale, branch-free buffer loads).  The partial-tile
 // V zeroing runs only on the last tile.
 // --------------------------------------------------------------------------
-template <class T, int D, int DV, int NW, int BN, int NQB, bool SPLIT = false>
+template <class T, int D, int DV, int NW, int BN, int NQB, bool SPLIT = false, bool WIDE = false>
 __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
@@ -466,7 +466,20 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     constexpr int VCH = (VTOT + NTH - 1) / NTH;
     static_assert(KTOT % NTH == 0 || KTOT < NTH, "tile split");
     static_assert(VTOT % NTH == 0 || VTOT < NTH, "tile split");
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 16];   // +16: dump slot
+    // WIDE: Q arrives by LDS-DMA (16-B coalesced loads, no VGPRs) into a [feature][BM
+    // tokens] image read back by transposed reads, and O leaves through the same image
+    // as 16-B row stores, instead of 2-byte gathers / scatters (one per feature and
+    // query).  The 32-B blocks of image row f are XOR-ed with (f & 3) | (bit 2 of f) << 2:
+    // conflict-free transposed reads (4 rows) and b16 writes (rows f, f + 4).
+    constexpr int ROWB = BM * 2;
+    constexpr int QOOFF = (2 * STAGE + 16 + 255) & ~255;
+    constexpr int QOB = WIDE ? (D > DV ? D : DV) * ROWB : 0;
+    __shared__ __attribute__((aligned(256))) char smem[QOOFF + QOB];   // +16 past the stages: dump slot
+    auto qo_at = [](int f, int byteoff) {
+        const int X = (f & 3) | (((f >> 2) & 1) << 2);
+        return f * ROWB + (((byteoff >> 5) ^ X) << 5) + (byteoff & 31);
+    };
+    char* const qoimg = smem + QOOFF;
 
     // K image swizzle: XOR the 32-B chunk index so that the 4 feature rows a
     // transposed read touches land on distinct banks (128-B rows: rows f and
@@ -488,8 +501,22 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
 
     int qiv[NQB];
     F8 qf[NQB][D / 16];
+    if constexpr (WIDE) {
+        static_assert(D * ROWB % (1024 * NW) == 0, "Q image DMA split");
 #pragma unroll
-    for (int u = 0; u < NQB; ++u) {
+        for (int it = 0; it < D * ROWB / 1024 / NW; ++it) {
+            const int k = it * NW + wave;
+            const int P = k * 1024 + lane * 16, f = P / ROWB, pb = P - f * ROWB;
+            const int X = (f & 3) | (((f >> 2) & 1) << 2);
+            const int lb = (((pb >> 5) ^ X) << 5) + (pb & 31);     // logical byte = 2 * token
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, (__attribute__((address_space(3))) void*)(qoimg + k * 1024), 16,
+                                                     (f * N + qb * BM) * 2 + lb, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < NQB; ++u) qiv[u] = qb * BM + (wave * NQB + u) * 32 + r;
+    }
+#pragma unroll
+    for (int u = 0; u < NQB && !WIDE; ++u) {
         qiv[u] = qb * BM + (wave * NQB + u) * 32 + r;
 #pragma unroll
         for (int s = 0; s < D / 16; ++s)
@@ -640,7 +667,19 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     const int jt0 = SPLIT ? split * p.tps : 0, jt1 = SPLIT ? min(NT, jt0 + p.tps) : NT;
     gload(jt0);
     lstore(buf0, jt0);
+    if constexpr (WIDE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's Q DMA landed
     __syncthreads();
+    if constexpr (WIDE) {
+#pragma unroll
+        for (int u = 0; u < NQB; ++u)
+#pragma unroll
+            for (int s = 0; s < D / 16; ++s) {
+                const int tb = ((wave * NQB + u) * 32 + 16 * kh + 4 * pp) * 2;
+                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(qoimg + qo_at(16 * s + 8 * h + qq, tb)));
+                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(qoimg + qo_at(16 * s + 8 * h + 4 + qq, tb)));
+                qf[u][s] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+    }
     for (int j = jt0; j < jt1; j += 2) {
         gload(min(j + 1, jt1 - 1));
         compute(buf0, buf0 + KBYTES, j);
@@ -679,6 +718,37 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         return;
     }
 
+    if constexpr (WIDE) {
+        // O (normalised, T) into the Q/O image, then one 16-B store per lane and row chunk
+#pragma unroll
+        for (int u = 0; u < NQB; ++u) {
+            const int qi = qiv[u];
+            const float lt = swap_halves_sum(l_run[u]);
+            const float inv = 1.0f / lt;
+            const int tb = ((wave * NQB + u) * 32 + r) * 2;
+#pragma unroll
+            for (int cb = 0; cb < DV / 32; ++cb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x)
+                    *(T*)(qoimg + qo_at(cb * 32 + acc_row(x, h), tb)) = (T)(oacc[u][cb][x] * inv);
+            if (qi < N && h == 0) {
+                p.m[(int64_t)b * N + qi] = m_true[u] * p.scale;
+                p.l[(int64_t)b * N + qi] = lt * exp2_fast((m_used[u] - m_true[u]) * c);
+            }
+        }
+        __syncthreads();
+        const auto ors = slab_rsrc((T*)p.O + (int64_t)b * N * dv, (uint32_t)(N * dv * (int)sizeof(T)));
+        constexpr int CPRO = ROWB / 16;
+        static_assert(DV * CPRO % NTH == 0, "O image store split");
+#pragma unroll
+        for (int it = 0; it < DV * CPRO / NTH; ++it) {
+            const int ch = it * NTH + tid, f = ch / CPRO, lb = (ch - f * CPRO) * 16;
+            const int q = qb * BM + lb / 2;
+            const u32x4 v4 = *(const u32x4*)(qoimg + qo_at(f, lb));
+            if (f < dv && q < N) __builtin_amdgcn_raw_buffer_store_b128(v4, ors, (f * N + q) * 2, 0, 0);
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < NQB; ++u) {
         const int qi = qiv[u];
@@ -709,6 +779,13 @@ template <class T, int D, int DV>
 __global__ __launch_bounds__(256, 2) void dense_fwd_w4q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 4, 64, 2>(p); }
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void dense_fwd_w8q2(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 2>(p); }
+// the default geometries with LDS-staged Q / O (N % 8 == 0, Q and O 16-B aligned)
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void dense_fwd_w8q2_wide(FwdParams p) {
+    dense_fwd_tiled<T, D, DV, 8, 64, 2, false, (D <= 64 && DV <= 64)>(p);   // the launcher picks it only there
+}
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void dense_fwd_w8b64_wide(FwdParams p) { dense_fwd_tiled<T, D, DV, 8, 64, 1, false, true>(p); }
 // occupancy variant: 32 query rows per wave, at least 4 waves per SIMD
 // (__launch_bounds__ second argument = minimum waves per SIMD: <= 128 VGPRs)
 template <class T, int D, int DV>
@@ -1081,7 +1158,10 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         // geometry per head-dim class (measured on MI355X):
         // <= 64: 8 waves x 2 query blocks (512 rows / workgroup); 128: 8 waves x 1.
         int v = g_fwd_variant;
-        if (v == 0) v = (D <= 64 && DVc <= 64) ? 7 : 5;
+        // default geometries stage Q / O through LDS when the shape allows (variant 20:
+        // the same geometries with per-element Q gathers / O stores, for A/B)
+        const bool wide = p.wide && (v == 0 || v == 5 || v == 7);
+        if (v == 0 || v == 20) v = (D <= 64 && DVc <= 64) ? 7 : 5;
         const int nw = (v == 4 || v == 6) ? 4 : 8;
         // query rows per workgroup (split kernels: 512 for w8q2 / t16q4, 256 for w8b64 / t16q2)
         const int rows = v == 8 ? 512 : v == 9 ? 256 : v == 16 ? 256 : 32 * nw * (v >= 6 ? 2 : 1);
@@ -1102,11 +1182,13 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         else if (q.nsplit > 1 && rows == 256) { FA_LAUNCH_T(dense_fwd_w8b64_split) }
         else if (q.nsplit > 1) { FA_LAUNCH_T(dense_fwd_w8q2_split) }
         else if (v == 4) { FA_LAUNCH_T(dense_fwd_w4b64) }
+        else if (v == 5 && wide) { FA_LAUNCH_T(dense_fwd_w8b64_wide) }
         else if (v == 5) { FA_LAUNCH_T(dense_fwd_w8b64) }
         else if (v == 6) { FA_LAUNCH_T(dense_fwd_w4q2) }
         else if (v == 8) { FA_LAUNCH_T(dense_fwd_t16q4) }
         else if (v == 9) { FA_LAUNCH_T(dense_fwd_t16q2) }
         else if (v == 16) { FA_LAUNCH_T(dense_fwd_w8b64_o4) }
+        else if (wide) { FA_LAUNCH_T(dense_fwd_w8q2_wide) }
         else { FA_LAUNCH_T(dense_fwd_w8q2) }
 #undef FA_LAUNCH_T
         if (q.nsplit > 1) {
@@ -1222,6 +1304,7 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
     const int epc = a.dtype == FA_DTYPE_F32 ? 4 : 8;
     p.ldk = (int)a.Nk;
     p.fast = (a.Nk % epc == 0) && aligned16(a.K) && aligned16(a.V);
+    p.wide = a.N % 8 == 0 && aligned16(a.Q) && aligned16(a.O);
     // bytes of the workspace taken by the padded K / V copies (0: none made)
     size_t pad_bytes = 0;
     if (!p.fast && a.workspace && fwd_pad_fits(a.dtype, a.Nk, a.d, a.dv, a.batch) &&

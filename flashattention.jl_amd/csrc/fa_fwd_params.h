@@ -24,6 +24,7 @@ struct FwdParams {
     float scale, scale_log2;
     float rescale_log2;   // lazy-rescale threshold (log2 units): kRescaleLog2, or the debug knob
     int fast;  // K/V rows 16-B aligned and Nk a multiple of the chunk width
+    int wide = 0;     // N % 8 == 0, Q and O 16-B aligned: Q / O staged through LDS (16-B accesses)
 };
 
 }  // namespace fa

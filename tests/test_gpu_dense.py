@@ -400,13 +400,14 @@ def test_forward_split_kv(fa, N, Nk, d, dv, B):
     assert_lm_close(_np(l1), _np(l2), "bfloat16", "l split vs unsplit")
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 16])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 16, 20])
 @pytest.mark.parametrize("N,Nk,d,dv,B,dtype", [(300, 200, 64, 64, 2, "bfloat16"), (513, 4100, 64, 32, 1, "bfloat16"),
                                                (256, 320, 128, 128, 2, "bfloat16"), (100, 72, 32, 64, 3, "float16"),
                                                (77, 136, 128, 64, 1, "float16"), (1024, 1024, 96, 96, 1, "bfloat16")])
 def test_forced_forward_variants(fa, variant, N, Nk, d, dv, B, dtype):
     """Every fast-kernel geometry (fa_debug_set_fwd_variant: 32x32x16 MFMA 4..7,
-    16x16x32 MFMA 8, 9) against the oracle, ragged Nk and dv != d included."""
+    16x16x32 MFMA 8, 9, 4 waves/SIMD 16, 20 the defaults with per-element Q / O
+    accesses) against the oracle, ragged Nk and dv != d included."""
     L = fa.lib()
     rng = np.random.default_rng(N * 7 + Nk + d * 3 + dv)
     cast = lambda a: torch.tensor(a).to(DT[dtype]).double().numpy()
@@ -421,6 +422,27 @@ def test_forced_forward_variants(fa, variant, N, Nk, d, dv, B, dtype):
     assert_close(_np(y), yr, dtype, f"y variant {variant}")
     assert_lm_close(_np(l), lr, dtype, "l")
     assert_lm_close(_np(m), mr, dtype, "m")
+
+
+@pytest.mark.parametrize("N,Nk,d,dv,B", [(4096, 4096, 64, 64, 32), (1000, 520, 64, 32, 128), (8, 64, 32, 32, 2),
+                                         (776, 1024, 128, 128, 64), (264, 200, 128, 64, 128), (1024, 512, 96, 96, 64)])
+def test_forward_lds_staged_q_o_bitwise(fa, N, Nk, d, dv, B):
+    """The default geometries stage Q (LDS-DMA) and O (16-B row stores) through an
+    LDS image when N % 8 == 0: bitwise equal to the per-element gathers / stores
+    (variant 20), partial last query block included.  Grids of >= 256 workgroups
+    (or one key tile), so neither run takes the split-KV path."""
+    L = fa.lib()
+    rng = np.random.default_rng(N + Nk * 3 + d)
+    Q, K, V = (fa.jl_tensor(rng.standard_normal(sh), torch.bfloat16) for sh in ((N, d, B), (Nk, d, B), (Nk, dv, B)))
+    a = [t.clone() for t in fa.dense_fa(Q, K, V)]
+    old = L.fa_debug_set_fwd_variant(20)
+    try:
+        b = fa.dense_fa(Q, K, V)
+        torch.cuda.synchronize()
+    finally:
+        L.fa_debug_set_fwd_variant(old)
+    for x, y, nm in zip(a, b, ("y", "l", "m")):
+        assert torch.equal(x, y), nm
 
 
 def test_empty_inputs(fa):
