@@ -376,7 +376,7 @@ def main():
                    "global_batch_heads": BH * world, "parallelism": f"shard(B*H) x{world}, no collective"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_BF16_TFLOPS, "traffic": _traffic_from_profiles(),
-                     "kernel": "fa::dense_fwd_w8q2<bf16,64,64>",
+                     "kernel": "fa::dense_fwd_w8q2_wide<bf16,64,64>",
                      "flops_per_launch": flops_rank, "avg_launch_ms": kern_s * 1e3},
         "settle": {"ms": settle_s * 1e3, "launches": settle_n,
                    "why": "untimed back-to-back launches so the GPU leaves its idle clock (DESIGN.md §6)"},

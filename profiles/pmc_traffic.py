@@ -15,7 +15,7 @@ import csv, glob, json, os, statistics, sys
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pmc = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out", "pmc")
 rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
-kern = sys.argv[3] if len(sys.argv) > 3 else "dense_fwd_w8q2"
+kern = sys.argv[3] if len(sys.argv) > 3 else "dense_fwd_w8q2_wide"
 vals = {}
 for f in glob.glob(os.path.join(pmc, "p*", "run_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
