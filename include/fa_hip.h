@@ -84,7 +84,12 @@ int fa_dense_fwd_ws(int dtype,
 size_t fa_dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
                               int64_t dv, int64_t batch);
 
-/* Workspace bytes fa_dense_bwd needs for these sizes (0 is a valid answer). */
+/* Workspace bytes fa_dense_bwd needs for these sizes (0 is a valid answer):
+ * 8·N·batch bytes of row statistics; for bf16 / fp16 shapes outside the MFMA
+ * kernels' set, zero-padded copies; and when the single-pass kernel applies
+ * (grids that fill the chip), per-slice counters plus the
+ * running fp32 dQ sums, 4·N·d·batch bytes.  A smaller workspace that still
+ * holds the first parts runs the two-pass form instead. */
 size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
                               int64_t dv, int64_t batch);
 
@@ -93,7 +98,8 @@ size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
  * src_cpp/FlashAttention.cpp:194-252):
  *   P = exp(s - m)/l, dV = P^T dO, dP = dO V^T, D = rowsum(dO .* O),
  *   dS = P .* (dP - D), dQ = scale dS K, dK = scale dS^T Q.
- * l, m are the forward's outputs.  dQ, dK, dV are fully written. */
+ * l, m are the forward's outputs.  dQ, dK, dV are fully written and bitwise
+ * reproducible (no atomics; the single pass sums dQ in a fixed order). */
 int fa_dense_bwd(int dtype,
                  const void* Q, const void* K, const void* V,
                  const void* O, const void* dO,

@@ -1,14 +1,18 @@
-"""configs[3] backward (4,16,8192,128) bf16 x 5 after a warm-up — a workload for rocprofv3."""
+"""configs[3] backward (8192, 128, 64 slabs) bf16, a fixed number of times in a given
+mode (fa_debug_set_bwd_mode; 0 auto = single pass) — a workload for PMC passes.
+Usage: python tools/exp/bwd_run.py [mode] [reps]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
 import torch, fa_hip
-from bench import _randn_jl
+mode = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+N, d, BH = 8192, 128, 64
 g = torch.Generator(device="cuda").manual_seed(1)
-N, d, BH = int(os.environ.get("FA_N", 8192)), int(os.environ.get("FA_D", 128)), 64
-Q, K, V, dO = (_randn_jl(fa_hip, (N, d, BH), torch.bfloat16, g) for _ in range(4))
+Q, K, V, dO = (fa_hip.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16) for _ in range(4))
 O, l, m = fa_hip.dense_fa(Q, K, V)
-for _ in range(int(os.environ.get("FA_REPS", 8))):
+fa_hip.lib().fa_debug_set_bwd_mode(mode)
+for _ in range(reps):
     fa_hip.dense_fa_backward(Q, K, V, O, dO, l, m)
 torch.cuda.synchronize()
-print("ok")
+print("ok", flush=True)
