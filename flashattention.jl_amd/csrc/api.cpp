@@ -122,10 +122,11 @@ int fa_debug_set_bwd_generic(int v) {
 // passes, 2 the single pass wherever its shape conditions hold, 3 as 2 with the
 // hand-off's timeout word preset, which exercises the dQ fallback pass; 4, 5, 6:
 // timing-only ablations of the single pass with WRONG dQ: no waits, no running-sum
-// traffic, neither; 7, 8: no running-sum loads / no running-sum stores).
+// traffic, neither; 7, 8: no running-sum loads / no running-sum stores; 9: no dS
+// image writes).
 int fa_debug_set_bwd_mode(int v) {
     const int old = fa::g_bwd_mode;
-    fa::g_bwd_mode = (v >= 1 && v <= 8) ? v : 0;
+    fa::g_bwd_mode = (v >= 1 && v <= 9) ? v : 0;
     return old;
 }
 

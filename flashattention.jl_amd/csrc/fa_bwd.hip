@@ -40,7 +40,7 @@ struct BwdParams {
     unsigned* err = nullptr;     // hand-off timeout flag (zeroed per call)
     float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
-    int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores
+    int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
 };
 
@@ -808,6 +808,14 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int sig32(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 
+// 16-B swizzle of the dSᵀ image, which is written by ds_write_b128 (8 groups of 8
+// contiguous lanes, banks mod 128 B) at rows sig32(r) and read only transposed.  A
+// write group covers rows {0..3} + {0, 8} (+ 4, 16, 20): the swizzle is a bijection of
+// row bits {0, 1, 3}, so its 8 slots differ; its bit 2 = row bit 1, so rows q and
+// q ^ 2 of a transposed read sit in opposite 64-B halves of their bank row.  (swz16
+// gives rows 0 and 4 the same slot: measured 6.7e7 conflict cycles at N = 8192.)
+__device__ __forceinline__ int swzds(int f) { return ((f >> 3) & 1) | ((f & 1) << 1) | (((f >> 1) & 1) << 2); }
+
 // [R rows][64 tokens] LDS image written by 8 waves (cf. dma_image).
 template <int R>
 __device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img, int ntok, int t0, int wave, int lane) {
@@ -899,6 +907,11 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     auto rowfrag = [&](const char* img, int cb, int tb, int s2) -> F8 {
         return *(const F8*)(img + (cb * 32 + r) * 128 + (((tb * 4 + 2 * s2 + h) ^ rsw) * 16));
     };
+    auto trat = [&](const char* a) -> F8 {   // transposed fragment at a per-lane address
+        const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+        const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
     auto slice_of = [&](int i) {
         int t = (i - OFF * j) % NS;
         return t < 0 ? t + NS : t;
@@ -950,6 +963,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const int ktb = wave & 1;
     const int dsrow = 32 * wave + sig32(r);                  // this lane's dSᵀ row
     const int cbq = wave % (D / 32), uq = wave / (D / 32);   // this wave's dQᵀ tile (wave < NTQ)
+    // transposed-read offset into the dSᵀ image (its own swizzle swzds; row 16 kk + 8h + qq)
+    const int trds = (8 * h + qq) * 128 + (((uq * 4 + kh * 2 + (sig >> 1)) ^ swzds(8 * h + qq)) * 16) + (sig & 1) * 8;
 
     int t_prev = 0, pos_prev = 0;
     bool pub_prev = false;
@@ -1002,8 +1017,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 for (int s2 = 0; s2 < 2; ++s2) dk[cb] = mfma32x32x16(rowfrag(qimg, cb, u, s2), dsf[s2], dk[cb]);
             // dSᵀ row kj: queries 32u + 16 s2 + 8h + {0..7}
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-                *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swz16(dsrow)) * 16)) = dsf[s2];
+            for (int s2 = 0; s2 < 2 && !(p.ablate & 32); ++s2)
+                *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow)) * 16)) = dsf[s2];
         }
 
         // running sum of the members before this one (sc1 loads, after B1; issuing
@@ -1030,7 +1045,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk)
-                acc = mfma32x32x16(rowfrag(kimg + (kk >> 2) * KSUB, cbq, (kk >> 1) & 1, kk & 1), trfrag(dsimg, uq, kk), acc);
+                acc = mfma32x32x16(rowfrag(kimg + (kk >> 2) * KSUB, cbq, (kk >> 1) & 1, kk & 1),
+                                   trat(dsimg + trds + 16 * kk * 128), acc);
             if (ldpin) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4)
@@ -1340,7 +1356,7 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             p.err = (unsigned*)(w + fz.flag_bytes - 256);
             p.part = (float*)(w + fz.flag_bytes);
             p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
-            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
+            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
             // mode 3 (tests): the timeout word starts set, so every poll gives up
             // and the guarded dQ pass must recompute dQ
             if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
@@ -1390,7 +1406,7 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             p.err = (unsigned*)(w + fz.flag_bytes - 256);
             p.part = (float*)(w + fz.flag_bytes);
             p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
-            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
+            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
             // mode 3 (tests): the timeout word starts set, so every poll gives up
             // and the guarded dQ pass must recompute dQ
             if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
