@@ -1,7 +1,8 @@
 """GPU parity of every fused windowed-forward kernel, each forced in turn
 (fa_debug_set_win_composed: 1 composed gather→dense→fold, 2 register-gather,
 3 one-window row-shift (ws <= 7) / row-scatter (ws = 8), 4 four-window
-row-staged, 5 one-window row-scatter, 6 two-window row-shift), against the oracle restatement of
+row-staged, 5 one-window row-scatter, 6 two-window row-shift, 7 / 8 two- / four-window LDS-DMA
+with rotated slots and analytic padding columns), against the oracle restatement of
 windowed_fa (src/windowed.jl:3-23, NNlib unfold/fold geometry) on geometries
 chosen for the row-staged kernels' edge handling: windows hanging over the
 left / right / bottom image edge, odd and even window x-starts (the row-shift
@@ -44,7 +45,7 @@ def _np(t):
     return t.detach().float().cpu().numpy().astype(np.float64)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
 def test_windowed_forced_path(fa, geom, path):
     W, H, ws, st, pad = geom

@@ -4,12 +4,13 @@ Build first (CPU): python tools/exp/win_stamp.py build"""
 import ctypes, os, subprocess, sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-SO = os.path.join(HERE, "libwin_stamp.so")
+ABL = int(os.environ.get("WABL", 0))   # FA_WIN_ABL of the stamped build (timing-only ablations)
+SO = os.path.join(HERE, f"libwin_stamp{ABL or ''}.so")
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     B = os.path.join(ROOT, "flashattention.jl_amd", "csrc", "build")
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-shared",
-                    "-fno-gpu-rdc", "-o", SO, "-x", "hip", os.path.join(HERE, "win_stamp.hip"), "-x", "none",
-                    os.path.join(B, "fa_fwd.hip.o"), os.path.join(B, "fa_bwd.hip.o")], check=True)
+                    "-fno-gpu-rdc", f"-DFA_WIN_ABL={ABL}", "-o", SO, "-x", "hip", os.path.join(HERE, "win_stamp.hip"),
+                    "-x", "none", os.path.join(B, "fa_fwd.hip.o"), os.path.join(B, "fa_bwd.hip.o")], check=True)
     sys.exit(0)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
 import numpy as np, torch, fa_hip
@@ -30,7 +31,8 @@ for rep in range(3):
         fa_hip.dense_fa_(O, fa_hip.jl_empty((N, 1, BH)), fa_hip.jl_empty((N, 1, BH)), Q, K, V)
     rc = L.stamp_run(P(q), P(k), P(v), P(y), P(l), P(m), Bimg, out.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0, rc
-    s = out.reshape(-1, 8).astype(np.int64)
+    nwg = (361 * Bimg + 1) // 2 if Bimg > 1 or os.environ.get("WPAIR") else 361 * Bimg
+    s = out.reshape(-1, 8).astype(np.int64)[:nwg]
     s[:, 1] = s[:, 0]          # the row-shift kernel has no stamp 1 (no separate zero-fill phase)
     ph = np.diff(s[:, :6], axis=1)
     rt0, rt1 = s[:, 6], s[:, 7]
@@ -39,4 +41,8 @@ for rep in range(3):
           ", ".join(f"{n}: {np.median(ph[:, i]):.0f}/{np.percentile(ph[:, i], 90):.0f}" for i, n in enumerate(names)))
     print(f"   WG total cycles median {np.median(s[:, 5] - s[:, 0]):.0f}; realtime (100 MHz ticks): WG span median "
           f"{np.median(rt1 - rt0):.0f}, first start -> last end {rt1.max() - rt0.min()}, "
-          f"start spread {rt0.max() - rt0.min()}", flush=True)
+          f"start spread {rt0.max() - rt0.min()}; sum of WG spans / (kernel span x 768 slots) "
+          f"{(rt1 - rt0).sum() / ((rt1.max() - rt0.min()) * 768):.2f}", flush=True)
+    if rep == 2:
+        span = np.percentile(rt1 - rt0, [10, 50, 90, 99])
+        print("   WG realtime span percentiles 10/50/90/99 (10 ns ticks):", span, flush=True)
