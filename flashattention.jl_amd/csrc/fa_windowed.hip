@@ -959,7 +959,7 @@ __device__ __forceinline__ int v_slot(int f, int w, int c) {
 }
 
 template <class T, int D, int DV, int NW>
-__global__ __launch_bounds__(256 * NW, NW == 4 ? 8 : 1) void win_dma(const T* __restrict__ q, const T* __restrict__ k,
+__global__ __launch_bounds__(256 * NW, 8) void win_dma(const T* __restrict__ q, const T* __restrict__ k,
                                                     const T* __restrict__ v, T* __restrict__ out,
                                                     float* __restrict__ lo, float* __restrict__ mo, WinDev g, int d,
                                                     int dv, int nwin_total, float scale, float scale_log2) {
@@ -967,7 +967,7 @@ __global__ __launch_bounds__(256 * NW, NW == 4 ? 8 : 1) void win_dma(const T* __
     typedef typename Frag8<T>::half F4;
     static_assert(NW == 2 || NW == 4, "windows per workgroup");
     constexpr int ROW = NW * 128, NWAVE = 4 * NW;
-    constexpr bool ALIAS = NW == 4 && DV <= D;          // V over the Q image
+    constexpr bool ALIAS = DV <= D;                     // V over the Q image
     constexpr int QIMG = D * ROW, VIMG = DV * ROW, VOFF = ALIAS ? 0 : 2 * QIMG;
     constexpr int LDSB = (VOFF + VIMG > 2 * QIMG) ? VOFF + VIMG : 2 * QIMG;
     constexpr int FPB = 1024 / ROW;                     // features per 1-KiB DMA block
