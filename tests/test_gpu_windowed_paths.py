@@ -184,3 +184,40 @@ def test_windowed_backward_f32_paths(fa, geom, path):
                 assert np.all(np.isfinite(x)) and err <= 2e-5, f"path {path} d {d} dv {dv} {nm}: {err:.2e}"
     finally:
         L.fa_debug_set_win_composed(old)
+
+
+@pytest.mark.parametrize("path", [0, 3, 6, 7, 8])
+def test_windowed_nonfinite_stays_in_its_window(fa, path):
+    """An inf in one pixel's k and v reaches only the window holding that pixel, as in
+    the reference, where windows are disjoint token sets.  The fused kernels load 8-pixel
+    rows that also hold a neighbour window's pixel (pixel 10 sits in the row load of
+    the window starting at 11); those slots must be masked (row-shift kernels: zeroed
+    in staging; LDS-DMA kernels: keys selected to -inf, V fragments ANDed with the slot
+    mask)."""
+    W, H, ws, st, pad = 32, 20, 7, 7, 3
+    rng = np.random.default_rng(5)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    d = dv = 64
+    q, k, v = (bf(rng.standard_normal((W, H, d, 1))) for _ in range(3))
+    k[10, 10, 5, 0] = np.inf
+    v[10, 10, 3, 0] = np.inf
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        y, l, m = fa.windowed_fa(*(fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v)), ws, stride=st, pad=pad)
+        torch.cuda.synchronize()
+    finally:
+        L.fa_debug_set_win_composed(old)
+    with np.errstate(invalid="ignore", over="ignore"):
+        yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
+    O0 = (W + 2 * pad - ws) // st + 1
+    inwin = np.zeros((W, H), bool)
+    inwin[4:11, 4:11] = True                      # window (1, 1): x, y in [4, 11)
+    # rows 18, 19 are covered by no window: NaN there in both (0/0, as the reference)
+    yo, yro = _np(y)[~inwin], yr[~inwin]
+    assert not np.isinf(yo).any(), f"path {path}: inf outside the window holding the inf"
+    assert_close(yo, yro, "bfloat16", f"y outside the window (path {path})", nan_ok=True)
+    keep = np.ones(lr.shape[2], bool)
+    keep[1 + O0 * 1] = False
+    assert_lm_close(_np(l)[:, :, keep], lr[:, :, keep], "bfloat16", f"l (path {path})")
+    assert_lm_close(_np(m)[:, :, keep], mr[:, :, keep], "bfloat16", f"m (path {path})")
