@@ -91,6 +91,41 @@ __global__ __launch_bounds__(256) void p8(uint4* y, size_t nlines) {
     }
 }
 
+// P9: a window pair (2 windows per 512-thread WG, as P1): 16-B stores of the aligned
+// chunks inside the pair's pixel span (lanes = (feature, row) per chunk), 2-B stores
+// (P1's lane pattern) for the pair's remaining pixels
+__global__ __launch_bounds__(512) void p9(unsigned short* y, int nwin) {
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5, wave = tid >> 6;
+    const int w0 = blockIdx.x * 2;
+    if (w0 + 1 >= nwin) return;
+    const int b = w0 / (OW * OW), rem = w0 % (OW * OW), wy = rem / OW, wx = rem % OW;
+    if (wx + 1 >= OW) return;                                     // pair in one row (timing only)
+    const int xs = wx * ST - PAD, y0 = wy * ST - PAD;
+    const int lo = xs < 0 ? 0 : xs, hi = min(xs + 2 * WS, W);   // pair's pixels [lo, hi)
+    const int c0 = (lo + 7) >> 3, c1 = hi >> 3;                   // full chunks [c0, c1)
+    // 16-B part: items (f, row j, chunk) over 512 threads
+    const int nfull = c1 > c0 ? c1 - c0 : 0;
+    for (int it = tid; it < C * WS * nfull; it += 512) {
+        const int f = it % C, rest = it / C, j = rest % WS, c = c0 + rest / WS;
+        const int py = y0 + j;
+        if (py < 0 || py >= H) continue;
+        *(uint4*)(y + (size_t)b * C * W * H + (size_t)f * W * H + (size_t)py * W + 8 * c) = make_uint4(it, it, it, it);
+    }
+    // 2-B part: P1's pattern, pixels outside the full chunks
+    const int wl = wave >> 2, qb = wave & 1, vc = (wave >> 1) & 1;
+    const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
+    const int px = xs + wl * WS + qtx, py = y0 + qty;
+    const bool full = px >= 8 * c0 && px < 8 * c1;
+    if (qtx < WS && qty < WS && px >= 0 && px < W && py >= 0 && py < H && !full) {
+        unsigned short* yb = y + (size_t)b * C * W * H + (size_t)py * W + px;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int cc = vc * 32 + (x & 3) + 8 * (x >> 2) + 4 * h;
+            yb[(size_t)cc * W * H] = (unsigned short)(x + w0);
+        }
+    }
+}
+
 int main() {
     const int B = 32, nwin = OW * OW * B;
     const size_t bytes = (size_t)B * C * W * H * 2;
@@ -118,6 +153,9 @@ int main() {
     const float t6 = time([&] { hipLaunchKernelGGL(p_rows<8>, dim3((nwin + 7) / 8), dim3(256), 0, 0, y, nwin); });
     const float t7 = time([&] { hipLaunchKernelGGL(p7, dim3(2048), dim3(256), 0, 0, (unsigned*)y, bytes / 4); });
     const float t8 = time([&] { hipLaunchKernelGGL(p8, dim3((unsigned)(bytes / 256 / 64)), dim3(256), 0, 0, (uint4*)y, bytes / 256); });
+    const float t9 = time([&] { hipLaunchKernelGGL(p9, dim3((nwin + 1) / 2), dim3(512), 0, 0, y, nwin); });
+    printf("P9 pair: 16-B owned chunks + 2-B rest %.1f us (pairs within one row only: ~%.0f %% of the bytes)\n", t9,
+           100.0 * 18 / 19);
     printf("P8 16-B, 64 lines per instruction (a line completed over 16 instructions of 4 waves) %.1f us\n", t8);
     printf("P4 b96+b16 rows, 1 window per WG %.1f us; P5 2 windows interleaved %.1f us; P6 8 windows interleaved %.1f us "
            "(interior windows only: ~%.0f %% of the bytes); P7 4-B streaming %.1f us\n", t4, t5, t6,
