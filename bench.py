@@ -359,7 +359,8 @@ def main():
 
     # cold: exactly W warm-up steps from idle, then the K timed steps
     wall_c, ev_c = time_region(step, args.steps, args.warmup, dist)
-    settle_n, settle_s = settle(step, args.settle_ms / 1e3)
+    with ClockSampler(torch.cuda.current_device()) as clk_settle:   # sustained load: many samples
+        settle_n, settle_s = settle(step, args.settle_ms / 1e3)
     with ClockSampler(torch.cuda.current_device()) as clk:
         wall, ev_s = time_region(step, args.steps, args.warmup, dist)
     value = flops_rank * world * args.steps / wall / 1e12
@@ -384,6 +385,10 @@ def main():
                  "avg_launch_ms": ev_c / args.steps * 1e3,
                  "what": "the same K steps after exactly W warm-up steps from idle, measured before settle"},
         "clock": clk.summary(),
+        # the timed region lasts a few ms, which holds one or two amdsmi samples (and the
+        # power reading averages over a longer window): the settle phase just before it
+        # runs the same launches back to back for --settle-ms and is sampled throughout
+        "clock_settle": clk_settle.summary(),
     }
 
     if not args.no_cfg5:
