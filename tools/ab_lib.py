@@ -68,6 +68,21 @@ for (N, d, BH) in [(4096, 64, 64), (8192, 128, 64)]:
     bench(f"dense N={N} d={d}", fwd, 4.0 * BH * N * N * d)
     del Q, K, V, O_
 
+if os.environ.get("AB_BWD"):   # dense backward (configs[3] and d = 64) and windowed forward / backward at B = 32
+    for (N, d, BH) in [(8192, 128, 64), (4096, 64, 64)]:
+        Q, K, V = mk((N, d, BH), 3)
+        dO = mk((N, d, BH), 4)[0]
+        O_, l, m = fa_hip.dense_fa(Q, K, V)
+
+        def bwd():
+            return fa_hip.dense_fa_backward(Q, K, V, O_, dO, l, m)
+        bench(f"dense bwd N={N} d={d}", bwd, 2.5 * 4.0 * BH * N * N * d)
+        del Q, K, V, dO, O_
+    q, k, v, dy = (fa_hip.jl_tensor(torch.randn((128, 128, 64, 32), device="cuda"), torch.bfloat16) for _ in range(4))
+    bench("windowed fwd B=32", lambda: fa_hip.windowed_fa(q, k, v, 7), 1.0)
+    y, lw, mw = fa_hip.windowed_fa(q, k, v, 7)
+    bench("windowed bwd B=32", lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), 1.0)
+
 if os.environ.get("AB_DENSE_ONLY"):
     sys.exit(0)
 N, d, BH, W = 16384, 64, 64, 129
