@@ -221,3 +221,49 @@ def test_windowed_nonfinite_stays_in_its_window(fa, path):
     keep[1 + O0 * 1] = False
     assert_lm_close(_np(l)[:, :, keep], lr[:, :, keep], "bfloat16", f"l (path {path})")
     assert_lm_close(_np(m)[:, :, keep], mr[:, :, keep], "bfloat16", f"m (path {path})")
+
+
+SEG_GEOMS = [  # width % 32 == 0 (the segment kernel's eligibility)
+    (32, 20, 7, 7, 3),
+    (64, 20, 7, 7, 3),
+    (64, 9, 7, 9, 0),       # stride > ws: uncovered columns and rows are NaN
+    (96, 13, 6, 6, 2),
+    (32, 30, 7, 8, 1),
+    (128, 16, 7, 7, 3),
+    (64, 8, 7, 7, 6),       # pad close to ws
+    (32, 12, 5, 5, 2),
+    (64, 17, 3, 3, 1),
+]
+
+
+@pytest.mark.parametrize("geom", SEG_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_segment_kernel(fa, geom):
+    """Mode 9 (win_seg: a workgroup owns a 32-pixel segment of a window row, computes every
+    window meeting it, stores y as 16-B chunks) vs the oracle, and bitwise vs the
+    register-staged two-window kernel (mode 6), which it follows window by window."""
+    W, H, ws, st, pad = geom
+    rng = np.random.default_rng(W * 31 + H * 7 + ws)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    L = fa.lib()
+    for (d, dv) in DIMS:
+        B = 3
+        q, k = (bf(rng.standard_normal((W, H, d, B))) for _ in range(2))
+        v = bf(rng.standard_normal((W, H, dv, B)))
+        outs = {}
+        for path in (9, 6):
+            old = L.fa_debug_set_win_composed(path)
+            try:
+                outs[path] = fa.windowed_fa(*(fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v)), ws,
+                                            stride=st, pad=pad)
+                torch.cuda.synchronize()
+            finally:
+                L.fa_debug_set_win_composed(old)
+        y, l, m = outs[9]
+        yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
+        tag = f"d {d} dv {dv}"
+        assert_close(_np(y), yr, "bfloat16", f"y ({tag})", nan_ok=True)
+        assert_lm_close(_np(l), lr, "bfloat16", f"l ({tag})")
+        assert_lm_close(_np(m), mr, "bfloat16", f"m ({tag})")
+        y6, l6, m6 = outs[6]
+        assert torch.equal(y.view(torch.int16), y6.view(torch.int16)), f"y not bitwise equal to mode 6 ({tag})"
+        assert torch.equal(l, l6) and torch.equal(m, m6), f"l, m not bitwise equal to mode 6 ({tag})"

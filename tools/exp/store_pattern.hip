@@ -126,6 +126,21 @@ __global__ __launch_bounds__(512) void p9(unsigned short* y, int nwin) {
     }
 }
 
+// P10: 16-B stores, a workgroup writes 64-B half lines (SEG = 32 px) or whole lines
+// (SEG = 64 px) of every (feature, row): lane -> (line, chunk), chunks fastest
+template <int SEG>
+__global__ __launch_bounds__(256) void p10(uint4* y, size_t nlines) {
+    constexpr int CPL = SEG / 8;                       // 16-B chunks per segment
+    const size_t seg0 = (size_t)blockIdx.x * 64;      // 64 segments per workgroup
+    for (int it = threadIdx.x; it < 64 * CPL; it += 256) {
+        const size_t sg = seg0 + it / CPL;            // segment index: (line, half)
+        const int c = it % CPL;
+        const size_t line = sg / (64 / SEG), part = sg % (64 / SEG);
+        // interleave: consecutive workgroups write the two halves of a line
+        if (line < nlines) y[line * 8 + part * CPL + c] = make_uint4(it, it, it, it);   // 8 chunks per 128-B line
+    }
+}
+
 int main() {
     const int B = 32, nwin = OW * OW * B;
     const size_t bytes = (size_t)B * C * W * H * 2;
@@ -154,6 +169,10 @@ int main() {
     const float t7 = time([&] { hipLaunchKernelGGL(p7, dim3(2048), dim3(256), 0, 0, (unsigned*)y, bytes / 4); });
     const float t8 = time([&] { hipLaunchKernelGGL(p8, dim3((unsigned)(bytes / 256 / 64)), dim3(256), 0, 0, (uint4*)y, bytes / 256); });
     const float t9 = time([&] { hipLaunchKernelGGL(p9, dim3((nwin + 1) / 2), dim3(512), 0, 0, y, nwin); });
+    const size_t nl = bytes / 128;
+    const float t10a = time([&] { hipLaunchKernelGGL(p10<32>, dim3((unsigned)(nl * 2 / 64)), dim3(256), 0, 0, (uint4*)y, nl); });
+    const float t10b = time([&] { hipLaunchKernelGGL(p10<64>, dim3((unsigned)(nl / 64)), dim3(256), 0, 0, (uint4*)y, nl); });
+    printf("P10 16-B chunks, workgroup-owned half lines %.1f us, whole lines %.1f us\n", t10a, t10b);
     printf("P9 pair: 16-B owned chunks + 2-B rest %.1f us (pairs within one row only: ~%.0f %% of the bytes)\n", t9,
            100.0 * 18 / 19);
     printf("P8 16-B, 64 lines per instruction (a line completed over 16 instructions of 4 waves) %.1f us\n", t8);
