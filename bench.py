@@ -476,6 +476,16 @@ def extra_benches(fa_hip, args, dist):
         res[f"{tag}_us"] = t * 1e6
         res[f"{tag}_GBs"] = Bc * Nc * (4 * dc * 2 + 8) / t / 1e9       # Q, K, V, O + l, m
         res[f"{tag}_tflops"] = 4.0 * Bc * Nc * Wc * dc / t / 1e12
+    # Float64 dense forward on the reference's own published cases
+    # (logs/compare1.txt:4,7: Julia Float64 CPU dense_fa at N=512 / 4096, d=64,
+    # bs=1: 2.392 / 28.64 ms) and on configs[0] (B·H = 4)
+    for (Nf, Bf) in ((512, 1), (512, 4), (4096, 1)):
+        Qf, Kf, Vf = (_randn_jl(fa_hip, (Nf, 64, Bf), torch.float64, gen) for _ in range(3))
+        Of = fa_hip.jl_empty((Nf, 64, Bf), torch.float64)
+        lf = fa_hip.jl_empty((Nf, 1, Bf)); mf = fa_hip.jl_empty((Nf, 1, Bf))
+        t = time_graph(lambda: fa_hip.dense_fa_(Of, lf, mf, Qf, Kf, Vf), args.steps, dist)
+        res[f"f64_dense_N{Nf}_d64_B{Bf}_us"] = t * 1e6
+        res[f"f64_dense_N{Nf}_d64_B{Bf}_gflops"] = 4.0 * Bf * Nf * Nf * 64 / t / 1e9
     # fused softmax: a configs[1]-shaped score tensor
     # (4096 x 4096 x 64 bf16, 2 GiB) along each dim; HBM-bound: read + write
     Ssm = _randn_jl(fa_hip, (4096, 4096, 64), torch.bfloat16, gen)

@@ -29,11 +29,19 @@ int ok() {
     return FA_OK;
 }
 
-bool valid_dtype(int dt) { return dt == FA_DTYPE_F32 || dt == FA_DTYPE_BF16 || dt == FA_DTYPE_F16; }
+bool valid_dtype(int dt) {
+    return dt == FA_DTYPE_F32 || dt == FA_DTYPE_BF16 || dt == FA_DTYPE_F16 || dt == FA_DTYPE_F64;
+}
 
 float resolve_scale(float scale, int64_t d) {
     if (!(scale > 0.0f) || !std::isfinite(scale)) return (float)(1.0 / std::sqrt((double)d));
     return scale;
+}
+// τ for the Float64 kernels: the default 1/√d in double (src/dense.jl:43), else the
+// caller's float scale widened.
+double resolve_scale64(float scale, int64_t d) {
+    if (!(scale > 0.0f) || !std::isfinite(scale)) return 1.0 / std::sqrt((double)d);
+    return (double)scale;
 }
 
 // Empty inputs, as dense_fa! (src/dense.jl:21-102) treats them: N = 0 or batch = 0
@@ -44,7 +52,7 @@ bool dense_fwd_empty(int dtype, void* O, float* l, float* m, int64_t N, int64_t 
     *rc = FA_OK;
     if (N == 0 || batch == 0) return true;
     if (Nk != 0) return false;
-    const size_t esz = dtype == FA_DTYPE_F32 ? 4 : 2;
+    const size_t esz = fa::dtype_size(dtype);
     if (!O || !l || !m) { *rc = FA_ERR_INVALID_ARG; return true; }
     if (hipMemsetAsync(O, 0, (size_t)(N * dv * batch) * esz, s) != hipSuccess ||
         hipMemsetAsync(l, 0, (size_t)(N * batch) * 4, s) != hipSuccess ||
@@ -169,6 +177,7 @@ int fa_dense_fwd_ws(int dtype, const void* Q, const void* K, const void* V, void
     if (need > 0 && (!workspace || workspace_bytes < need))
         return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_dense_fwd_workspace()");
     fa::DenseArgs a{dtype, Q, K, V, O, l, m, N, Nk, d, dv, batch, resolve_scale(scale, d)};
+    a.scale64 = resolve_scale64(scale, d);
     a.workspace = workspace;
     a.workspace_bytes = workspace_bytes;
     const char* why = "";
@@ -188,6 +197,7 @@ int fa_dense_fwd(int dtype, const void* Q, const void* K, const void* V, void* O
         return erc == FA_OK ? ok() : fail(erc, fn, erc == FA_ERR_HIP ? "hipMemsetAsync failed" : "null pointer");
     if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     fa::DenseArgs a{dtype, Q, K, V, O, l, m, N, Nk, d, dv, batch, resolve_scale(scale, d)};
+    a.scale64 = resolve_scale64(scale, d);
     const char* why = "";
     const int rc = fa::launch_dense_fwd(a, (hipStream_t)hip_stream, &why);
     return rc == FA_OK ? ok() : fail(rc, fn, why);
@@ -207,7 +217,7 @@ int fa_dense_bwd(int dtype, const void* Q, const void* K, const void* V, const v
     if (N < 0 || Nk < 0 || d < 1 || dv < 1 || batch < 0)
         return fail(FA_ERR_INVALID_ARG, fn, "DimensionMismatch: N, Nk, batch must be >= 0 and d, dv >= 1");
     if (N == 0 || Nk == 0 || batch == 0) {   // empty sums: every gradient element is 0
-        const size_t esz = dtype == FA_DTYPE_F32 ? 4 : 2;
+        const size_t esz = fa::dtype_size(dtype);
         const hipStream_t s = (hipStream_t)hip_stream;
         const size_t nq = (size_t)(N * d * batch), nk = (size_t)(Nk * d * batch), nv = (size_t)(Nk * dv * batch);
         if ((nq && !dQ) || (nk && (!dK || !dV))) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
@@ -224,6 +234,7 @@ int fa_dense_bwd(int dtype, const void* Q, const void* K, const void* V, const v
         return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_dense_bwd_workspace()");
     fa::DenseBwdArgs a{dtype, Q, K, V, O, dO, l, m, dQ, dK, dV, N, Nk, d, dv, batch,
                        resolve_scale(scale, d), workspace, workspace_bytes};
+    a.scale64 = resolve_scale64(scale, d);
     const char* why = "";
     const int rc = fa::launch_dense_bwd(a, (hipStream_t)hip_stream, &why);
     return rc == FA_OK ? ok() : fail(rc, fn, why);
@@ -264,6 +275,7 @@ int fa_windowed_fwd(int dtype, const void* q, const void* k, const void* v, void
     a.dtype = dtype; a.q = q; a.k = k; a.v = v; a.y = y; a.l = l; a.m = m;
     a.d = d; a.dv = dv; a.batch = batch;
     a.scale = resolve_scale(scale, d);
+    a.scale64 = resolve_scale64(scale, d);
     const size_t need = fa::windowed_fwd_workspace(dtype, a.g, d, dv, batch);
     if (need > 0 && (!workspace || workspace_bytes < need))
         return fail(FA_ERR_WORKSPACE, fn, "workspace missing or smaller than fa_windowed_fwd_workspace()");
@@ -323,6 +335,7 @@ int fa_windowed_bwd(int dtype, const void* q, const void* k, const void* v, cons
     a.dq = dq; a.dk = dk; a.dv_ = dv_;
     a.d = d; a.dv = dv; a.batch = batch;
     a.scale = resolve_scale(scale, d);
+    a.scale64 = resolve_scale64(scale, d);
     a.workspace = workspace;
     a.workspace_bytes = workspace_bytes;
     rc = fa::launch_windowed_bwd(a, (hipStream_t)hip_stream, &why);
@@ -340,6 +353,7 @@ int fa_circulant_fwd(int dtype, const void* Q, const void* K, const void* V, voi
     if (N == 0 || batch == 0) return ok();   // circulant_fa! loops over no row / slab
     if (!Q || !K || !V || !O || !l || !m) return fail(FA_ERR_INVALID_ARG, fn, "null pointer");
     fa::CircArgs a{dtype, Q, K, V, O, l, m, N, d, dv, batch, W, resolve_scale(scale, d)};
+    a.scale64 = resolve_scale64(scale, d);
     const char* why = "";
     const int rc = fa::launch_circulant_fwd(a, (hipStream_t)hip_stream, &why);
     return rc == FA_OK ? ok() : fail(rc, fn, why);

@@ -35,6 +35,7 @@ struct BwdParams {
     int N, Nk, d, dv, batch;
     int nblk, total_wg;          // fast path: row blocks per slab, workgroups
     float scale, scale_log2;
+    double scale64 = 0.0;        // Float64 generic path: τ in double
     // single-pass kernel (bwd_fused): dQ hand-off state, all in the caller's workspace
     unsigned* flags = nullptr;   // [batch][nqt] members that have published slice t (zeroed per call)
     unsigned* err = nullptr;     // hand-off timeout flag (zeroed per call)
@@ -108,21 +109,36 @@ __global__ __launch_bounds__(256) void bwd_prepass_v(BwdParams p) {
 }
 
 // --------------------------------------------------------------------------
-// 2./3. generic SIMT path.  Tiles of 32 queries x 32 keys in LDS (fp32).
+// 2./3. generic SIMT path.  Tiles of 32 queries x 32 keys in LDS, arithmetic in
+// A: float for the 16/32-bit types, double for Float64 (whose row statistics
+// nD / nlse are double too, fa_f64.hip).  LDS rows hold d + 1 (dv + 1) elements,
+// so the per-key / per-query row reads of 32 lanes fall in distinct banks.
 // --------------------------------------------------------------------------
 constexpr int kGT = 32;          // tile edge
 constexpr int kGThreads = 256;
 
+__device__ __forceinline__ float fma_a(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double fma_a(double a, double b, double c) { return fma(a, b, c); }
+__device__ __forceinline__ float exp2_a(float x) { return exp2f(x); }
+__device__ __forceinline__ double exp2_a(double x) { return exp2(x); }
+template <class A> __device__ __forceinline__ A bscale(const BwdParams& p) {
+    if constexpr (sizeof(A) == 8) return p.scale64; else return p.scale;
+}
+template <class A> __device__ __forceinline__ A bscale_log2(const BwdParams& p) {
+    if constexpr (sizeof(A) == 8) return p.scale64 * 1.4426950408889634074; else return p.scale_log2;
+}
+
 // dQ: one block per (b, 32-query tile).
-template <class T>
+template <class T, class A>
 __global__ __launch_bounds__(kGThreads) void bwd_generic_dq(BwdParams p) {
-    extern __shared__ __attribute__((aligned(16))) float gsm[];
-    const int d = p.d, dv = p.dv, N = p.N, Nk = p.Nk;
-    float* sQ = gsm;                     // [32][d]
-    float* sdO = sQ + kGT * d;           // [32][dv]
-    float* sK = sdO + kGT * dv;          // [32][d]
-    float* sV = sK + kGT * d;            // [32][dv]
-    float* sdS = sV + kGT * dv;          // [32 q][33]
+    extern __shared__ __attribute__((aligned(16))) char gsm_raw[];
+    A* const gsm = (A*)gsm_raw;
+    const int d = p.d, dv = p.dv, N = p.N, Nk = p.Nk, ld = d + 1, ldv = dv + 1;
+    A* sQ = gsm;                         // [32][d+1]
+    A* sdO = sQ + kGT * ld;              // [32][dv+1]
+    A* sK = sdO + kGT * ldv;             // [32][d+1]
+    A* sV = sK + kGT * ld;               // [32][dv+1]
+    A* sdS = sV + kGT * ldv;             // [32 q][33]
     const int nqt = (N + kGT - 1) / kGT;
     const int b = blockIdx.x / nqt, q0 = (blockIdx.x % nqt) * kGT;
     const int tid = threadIdx.x;
@@ -132,38 +148,39 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dq(BwdParams p) {
     const T* dOb = (const T*)p.dO + (int64_t)b * N * dv;
     for (int i = tid; i < kGT * d; i += kGThreads) {
         const int q = i % kGT, f = i / kGT;
-        sQ[q * d + f] = (q0 + q < N) ? to_f(Qb[(int64_t)f * N + q0 + q]) : 0.0f;
+        sQ[q * ld + f] = (q0 + q < N) ? (A)Qb[(int64_t)f * N + q0 + q] : (A)0;
     }
     for (int i = tid; i < kGT * dv; i += kGThreads) {
         const int q = i % kGT, f = i / kGT;
-        sdO[q * dv + f] = (q0 + q < N) ? to_f(dOb[(int64_t)f * N + q0 + q]) : 0.0f;
+        sdO[q * ldv + f] = (q0 + q < N) ? (A)dOb[(int64_t)f * N + q0 + q] : (A)0;
     }
     // each thread owns dQ entries (q, f) = (i % 32, i / 32) for i = tid + 256·t
     constexpr int kMaxPer = 128 * kGT / kGThreads;   // d <= 128
-    float acc[kMaxPer];
+    A acc[kMaxPer];
 #pragma unroll
-    for (int t = 0; t < kMaxPer; ++t) acc[t] = 0.0f;
-    const float* nD = p.nD + (int64_t)b * N;
-    const float* nL = p.nlse + (int64_t)b * N;
+    for (int t = 0; t < kMaxPer; ++t) acc[t] = (A)0;
+    const A* nD = (const A*)p.nD + (int64_t)b * N;
+    const A* nL = (const A*)p.nlse + (int64_t)b * N;
+    const A sl2 = bscale_log2<A>(p);
     for (int k0 = 0; k0 < Nk; k0 += kGT) {
         __syncthreads();
         for (int i = tid; i < kGT * d; i += kGThreads) {
             const int k = i % kGT, f = i / kGT;
-            sK[k * d + f] = (k0 + k < Nk) ? to_f(Kb[(int64_t)f * Nk + k0 + k]) : 0.0f;
+            sK[k * ld + f] = (k0 + k < Nk) ? (A)Kb[(int64_t)f * Nk + k0 + k] : (A)0;
         }
         for (int i = tid; i < kGT * dv; i += kGThreads) {
             const int k = i % kGT, f = i / kGT;
-            sV[k * dv + f] = (k0 + k < Nk) ? to_f(Vb[(int64_t)f * Nk + k0 + k]) : 0.0f;
+            sV[k * ldv + f] = (k0 + k < Nk) ? (A)Vb[(int64_t)f * Nk + k0 + k] : (A)0;
         }
         __syncthreads();
         for (int e = tid; e < kGT * kGT; e += kGThreads) {
             const int q = e / kGT, k = e % kGT;
-            float ds = 0.0f;
+            A ds = (A)0;
             if (q0 + q < N && k0 + k < Nk) {
-                float s = 0.0f, dp = 0.0f;
-                for (int f = 0; f < d; ++f) s = fmaf(sQ[q * d + f], sK[k * d + f], s);
-                for (int f = 0; f < dv; ++f) dp = fmaf(sdO[q * dv + f], sV[k * dv + f], dp);
-                const float pr = exp2f((s + nL[q0 + q]) * p.scale_log2);
+                A s = (A)0, dp = (A)0;
+                for (int f = 0; f < d; ++f) s = fma_a(sQ[q * ld + f], sK[k * ld + f], s);
+                for (int f = 0; f < dv; ++f) dp = fma_a(sdO[q * ldv + f], sV[k * ldv + f], dp);
+                const A pr = exp2_a((s + nL[q0 + q]) * sl2);
                 ds = pr * (dp + nD[q0 + q]);
             }
             sdS[q * (kGT + 1) + k] = ds;
@@ -173,31 +190,33 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dq(BwdParams p) {
         for (int t = 0; t < kMaxPer; ++t) {
             const int i = tid + kGThreads * t, q = i % kGT, f = i / kGT;
             if (f < d) {
-                float a = acc[t];
-                for (int k = 0; k < kGT; ++k) a = fmaf(sdS[q * (kGT + 1) + k], sK[k * d + f], a);
+                A a = acc[t];
+                for (int k = 0; k < kGT; ++k) a = fma_a(sdS[q * (kGT + 1) + k], sK[k * ld + f], a);
                 acc[t] = a;
             }
         }
     }
     T* dQb = (T*)p.dQ + (int64_t)b * N * d;
+    const A sc = bscale<A>(p);
 #pragma unroll
     for (int t = 0; t < kMaxPer; ++t) {
         const int i = tid + kGThreads * t, q = i % kGT, f = i / kGT;
-        if (f < d && q0 + q < N) dQb[(int64_t)f * N + q0 + q] = (T)(acc[t] * p.scale);
+        if (f < d && q0 + q < N) dQb[(int64_t)f * N + q0 + q] = (T)(acc[t] * sc);
     }
 }
 
 // dK, dV: one block per (b, 32-key tile).
-template <class T>
+template <class T, class A>
 __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
-    extern __shared__ __attribute__((aligned(16))) float gsm[];
-    const int d = p.d, dv = p.dv, N = p.N, Nk = p.Nk;
-    float* sK = gsm;                     // [32][d]
-    float* sV = sK + kGT * d;            // [32][dv]
-    float* sQ = sV + kGT * dv;           // [32][d]
-    float* sdO = sQ + kGT * d;           // [32][dv]
-    float* sP = sdO + kGT * dv;          // [32 q][33]
-    float* sdS = sP + kGT * (kGT + 1);   // [32 q][33]
+    extern __shared__ __attribute__((aligned(16))) char gsm_raw[];
+    A* const gsm = (A*)gsm_raw;
+    const int d = p.d, dv = p.dv, N = p.N, Nk = p.Nk, ld = d + 1, ldv = dv + 1;
+    A* sK = gsm;                         // [32][d+1]
+    A* sV = sK + kGT * ld;               // [32][dv+1]
+    A* sQ = sV + kGT * ldv;              // [32][d+1]
+    A* sdO = sQ + kGT * ld;              // [32][dv+1]
+    A* sP = sdO + kGT * ldv;             // [32 q][33]
+    A* sdS = sP + kGT * (kGT + 1);       // [32 q][33]
     const int nkt = (Nk + kGT - 1) / kGT;
     const int b = blockIdx.x / nkt, k0 = (blockIdx.x % nkt) * kGT;
     const int tid = threadIdx.x;
@@ -207,37 +226,38 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
     const T* dOb = (const T*)p.dO + (int64_t)b * N * dv;
     for (int i = tid; i < kGT * d; i += kGThreads) {
         const int k = i % kGT, f = i / kGT;
-        sK[k * d + f] = (k0 + k < Nk) ? to_f(Kb[(int64_t)f * Nk + k0 + k]) : 0.0f;
+        sK[k * ld + f] = (k0 + k < Nk) ? (A)Kb[(int64_t)f * Nk + k0 + k] : (A)0;
     }
     for (int i = tid; i < kGT * dv; i += kGThreads) {
         const int k = i % kGT, f = i / kGT;
-        sV[k * dv + f] = (k0 + k < Nk) ? to_f(Vb[(int64_t)f * Nk + k0 + k]) : 0.0f;
+        sV[k * ldv + f] = (k0 + k < Nk) ? (A)Vb[(int64_t)f * Nk + k0 + k] : (A)0;
     }
     constexpr int kMaxPer = 128 * kGT / kGThreads;
-    float accK[kMaxPer], accV[kMaxPer];
+    A accK[kMaxPer], accV[kMaxPer];
 #pragma unroll
-    for (int t = 0; t < kMaxPer; ++t) { accK[t] = 0.0f; accV[t] = 0.0f; }
-    const float* nD = p.nD + (int64_t)b * N;
-    const float* nL = p.nlse + (int64_t)b * N;
+    for (int t = 0; t < kMaxPer; ++t) { accK[t] = (A)0; accV[t] = (A)0; }
+    const A* nD = (const A*)p.nD + (int64_t)b * N;
+    const A* nL = (const A*)p.nlse + (int64_t)b * N;
+    const A sl2 = bscale_log2<A>(p);
     for (int q0 = 0; q0 < N; q0 += kGT) {
         __syncthreads();
         for (int i = tid; i < kGT * d; i += kGThreads) {
             const int q = i % kGT, f = i / kGT;
-            sQ[q * d + f] = (q0 + q < N) ? to_f(Qb[(int64_t)f * N + q0 + q]) : 0.0f;
+            sQ[q * ld + f] = (q0 + q < N) ? (A)Qb[(int64_t)f * N + q0 + q] : (A)0;
         }
         for (int i = tid; i < kGT * dv; i += kGThreads) {
             const int q = i % kGT, f = i / kGT;
-            sdO[q * dv + f] = (q0 + q < N) ? to_f(dOb[(int64_t)f * N + q0 + q]) : 0.0f;
+            sdO[q * ldv + f] = (q0 + q < N) ? (A)dOb[(int64_t)f * N + q0 + q] : (A)0;
         }
         __syncthreads();
         for (int e = tid; e < kGT * kGT; e += kGThreads) {
             const int q = e / kGT, k = e % kGT;
-            float pr = 0.0f, ds = 0.0f;
+            A pr = (A)0, ds = (A)0;
             if (q0 + q < N && k0 + k < Nk) {
-                float s = 0.0f, dp = 0.0f;
-                for (int f = 0; f < d; ++f) s = fmaf(sQ[q * d + f], sK[k * d + f], s);
-                for (int f = 0; f < dv; ++f) dp = fmaf(sdO[q * dv + f], sV[k * dv + f], dp);
-                pr = exp2f((s + nL[q0 + q]) * p.scale_log2);
+                A s = (A)0, dp = (A)0;
+                for (int f = 0; f < d; ++f) s = fma_a(sQ[q * ld + f], sK[k * ld + f], s);
+                for (int f = 0; f < dv; ++f) dp = fma_a(sdO[q * ldv + f], sV[k * ldv + f], dp);
+                pr = exp2_a((s + nL[q0 + q]) * sl2);
                 ds = pr * (dp + nD[q0 + q]);
             }
             sP[q * (kGT + 1) + k] = pr;
@@ -248,24 +268,25 @@ __global__ __launch_bounds__(kGThreads) void bwd_generic_dkdv(BwdParams p) {
         for (int t = 0; t < kMaxPer; ++t) {
             const int i = tid + kGThreads * t, k = i % kGT, f = i / kGT;
             if (f < d) {
-                float a = accK[t];
-                for (int q = 0; q < kGT; ++q) a = fmaf(sdS[q * (kGT + 1) + k], sQ[q * d + f], a);
+                A a = accK[t];
+                for (int q = 0; q < kGT; ++q) a = fma_a(sdS[q * (kGT + 1) + k], sQ[q * ld + f], a);
                 accK[t] = a;
             }
             if (f < dv) {
-                float a = accV[t];
-                for (int q = 0; q < kGT; ++q) a = fmaf(sP[q * (kGT + 1) + k], sdO[q * dv + f], a);
+                A a = accV[t];
+                for (int q = 0; q < kGT; ++q) a = fma_a(sP[q * (kGT + 1) + k], sdO[q * ldv + f], a);
                 accV[t] = a;
             }
         }
     }
     T* dKb = (T*)p.dK + (int64_t)b * Nk * d;
     T* dVb = (T*)p.dV + (int64_t)b * Nk * dv;
+    const A sc = bscale<A>(p);
 #pragma unroll
     for (int t = 0; t < kMaxPer; ++t) {
         const int i = tid + kGThreads * t, k = i % kGT, f = i / kGT;
         if (k0 + k < Nk) {
-            if (f < d) dKb[(int64_t)f * Nk + k0 + k] = (T)(accK[t] * p.scale);
+            if (f < d) dKb[(int64_t)f * Nk + k0 + k] = (T)(accK[t] * sc);
             if (f < dv) dVb[(int64_t)f * Nk + k0 + k] = (T)accV[t];
         }
     }
@@ -1153,7 +1174,7 @@ static hipError_t launch_fast(const BwdParams& p, hipStream_t s) {
 // --------------------------------------------------------------------------
 static bool cls_dim(int64_t x) { return x == 32 || x == 64 || x == 128; }
 static bool shape_fast(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv) {
-    return dtype != FA_DTYPE_F32 && cls_dim(d) && cls_dim(dv) && N % 8 == 0 && Nk % 8 == 0 &&
+    return dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_F64 && cls_dim(d) && cls_dim(dv) && N % 8 == 0 && Nk % 8 == 0 &&
            N * d * 2 < INT32_MAX && Nk * d * 2 < INT32_MAX && N * dv * 2 < INT32_MAX && Nk * dv * 2 < INT32_MAX;
 }
 struct BwdPad {
@@ -1164,7 +1185,9 @@ struct BwdPad {
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     BwdPad pl;
-    if (dtype == FA_DTYPE_F32 || d > kMaxHeadDim || dv > kMaxHeadDim || shape_fast(dtype, N, Nk, d, dv)) return pl;
+    if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || d > kMaxHeadDim || dv > kMaxHeadDim ||
+        shape_fast(dtype, N, Nk, d, dv))
+        return pl;
     pl.Np = (N + 7) / 8 * 8;
     pl.Nkp = (Nk + 7) / 8 * 8;
     pl.Dp = head_dim_class(d);
@@ -1199,7 +1222,7 @@ static int device_cus() {
 }
 static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     FusedPlan f;
-    if (dtype == FA_DTYPE_F32 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
+    if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
     const int cus = device_cus();
     if (cus < 8 || 3 * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
@@ -1214,6 +1237,7 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
 }
 
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+    if (dtype == FA_DTYPE_F64) return (size_t)(2 * N * batch * sizeof(double) + 256);   // nD, nlse in double
     const BwdPad pl = pad_plan(dtype, N, Nk, d, dv, batch);
     const int64_t rows = pl.on ? pl.Np : N;
     const FusedPlan fz = pl.on ? fused_plan(dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp, batch)
@@ -1273,17 +1297,18 @@ static hipError_t unpad_launch(const void* src, void* dst, int64_t N, int64_t C,
     return hipGetLastError();
 }
 
-template <class T>
+template <class T, class A = float>
 static hipError_t launch_generic(const BwdParams& p, hipStream_t s) {
     const int64_t nq = ((int64_t)p.N + kGT - 1) / kGT * p.batch;
     const int64_t nk = ((int64_t)p.Nk + kGT - 1) / kGT * p.batch;
-    const size_t sm_dq = sizeof(float) * (kGT * (2 * p.d + 2 * p.dv) + kGT * (kGT + 1));
-    const size_t sm_kv = sizeof(float) * (kGT * (2 * p.d + 2 * p.dv) + 2 * kGT * (kGT + 1));
+    const size_t rows = kGT * (2 * (p.d + 1) + 2 * (p.dv + 1));
+    const size_t sm_dq = sizeof(A) * (rows + kGT * (kGT + 1));
+    const size_t sm_kv = sizeof(A) * (rows + 2 * kGT * (kGT + 1));
     // > 64 KiB of dynamic LDS at d = dv = 128 (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute((const void*)bwd_generic_dq<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm_dq);
-    (void)hipFuncSetAttribute((const void*)bwd_generic_dkdv<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm_kv);
-    hipLaunchKernelGGL(bwd_generic_dq<T>, dim3((unsigned)nq), dim3(kGThreads), sm_dq, s, p);
-    hipLaunchKernelGGL(bwd_generic_dkdv<T>, dim3((unsigned)nk), dim3(kGThreads), sm_kv, s, p);
+    (void)hipFuncSetAttribute((const void*)bwd_generic_dq<T, A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm_dq);
+    (void)hipFuncSetAttribute((const void*)bwd_generic_dkdv<T, A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm_kv);
+    hipLaunchKernelGGL((bwd_generic_dq<T, A>), dim3((unsigned)nq), dim3(kGThreads), sm_dq, s, p);
+    hipLaunchKernelGGL((bwd_generic_dkdv<T, A>), dim3((unsigned)nk), dim3(kGThreads), sm_kv, s, p);
     return hipGetLastError();
 }
 
@@ -1327,10 +1352,30 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     p.N = (int)a.N; p.Nk = (int)a.Nk; p.d = (int)a.d; p.dv = (int)a.dv; p.batch = (int)a.batch;
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
+    hipError_t e;
+    if (a.dtype == FA_DTYPE_F64) {
+        // Float64: row statistics recomputed in double (not from the float32 l, m),
+        // then the SIMT passes in double
+        if (a.workspace_bytes < dense_bwd_workspace(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch)) {
+            *why = "workspace smaller than fa_dense_bwd_workspace()";
+            return FA_ERR_WORKSPACE;
+        }
+        double* nD = (double*)ws;
+        double* nlse = nD + a.N * a.batch;
+        p.nD = (float*)nD;
+        p.nlse = (float*)nlse;
+        p.scale64 = a.scale64 > 0.0 ? a.scale64 : (double)a.scale;
+        const int rc = launch_f64_bwd_stats(a, nD, nlse, s, why);
+        if (rc != FA_OK) return rc;
+        if ((e = launch_generic<double, double>(p, s)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
+        return FA_OK;
+    }
     const bool fast = !g_bwd_force_generic && shape_fast(a.dtype, a.N, a.Nk, a.d, a.dv) &&
                       aligned16(a.Q) && aligned16(a.K) && aligned16(a.V) && aligned16(a.dO);
     const BwdPad pl = pad_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
-    hipError_t e;
     if (!fast && pl.on && !g_bwd_force_generic) {
         // padded fast path: workspace = [nD | nlse] (Np rows) then the padded slabs
         const int64_t B = a.batch;

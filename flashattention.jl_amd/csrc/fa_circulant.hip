@@ -104,6 +104,59 @@ __global__ __launch_bounds__(256) void circ_fwd_generic(CircParams P) {
     }
 }
 
+// Float64 (the reference's test element type): the same one-wave-per-query sweep
+// in double, exact online softmax (no lazy rescale), τ resolved in double.
+__global__ __launch_bounds__(256) void circ_fwd_f64(CircParams P, double scale, int64_t batch) {
+    const int lane = threadIdx.x & 63;
+    const int64_t gq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int N = P.N, d = P.d, dv = P.dv, W = P.W;
+    if (gq >= (int64_t)N * batch) return;
+    const int b = (int)(gq / N), i = (int)(gq - (int64_t)b * N);
+    const double* Q = (const double*)P.Q + (int64_t)b * N * d;
+    const double* K = (const double*)P.K + (int64_t)b * N * d;
+    const double* V = (const double*)P.V + (int64_t)b * N * dv;
+    double qv[2], acc[2] = {0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int f = lane + 64 * u;
+        qv[u] = f < d ? Q[(int64_t)f * N + i] : 0.0;
+    }
+    double m = -__builtin_huge_val(), l = 0.0;
+    int key = ((i - P.p) % N + N) % N;
+    for (int t = 0; t < W; ++t) {
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int f = lane + 64 * u;
+            if (f < d) s = fma(qv[u], K[(int64_t)f * N + key], s);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        s *= scale;
+        const double mn = __builtin_elementwise_maximum(m, s);
+        const double a = exp(m - mn);   // m = −inf first: exp(−inf) = 0
+        const double pr = exp(s - mn);
+        l = l * a + pr;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int cc = lane + 64 * u;
+            acc[u] = acc[u] * a + (cc < dv ? pr * V[(int64_t)cc * N + key] : 0.0);
+        }
+        m = mn;
+        key = key + 1 == N ? 0 : key + 1;
+    }
+    double* O = (double*)P.O + (int64_t)b * N * dv;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int cc = lane + 64 * u;
+        if (cc < dv) O[(int64_t)cc * N + i] = acc[u] / l;
+    }
+    if (lane == 0) {
+        P.m[(int64_t)b * N + i] = (float)m;
+        P.l[(int64_t)b * N + i] = (float)l;
+    }
+}
+
 // --------------------------------------------------------------------------
 // LDS-tiled SIMT kernel (every dtype incl. fp32, any N / alignment): one thread
 // per query, 256 consecutive queries per workgroup.  The union of their bands,
@@ -466,7 +519,7 @@ int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why) {
         *why = "head dimension exceeds the compiled maximum (128)";
         return FA_ERR_UNSUPPORTED;
     }
-    const int64_t esz = a.dtype == FA_DTYPE_F32 ? 4 : 2;
+    const int64_t esz = (int64_t)dtype_size(a.dtype);
     if (a.N * a.d * esz >= (int64_t)INT32_MAX || a.N * a.dv * esz >= (int64_t)INT32_MAX ||
         a.W > INT32_MAX / 2 || a.N * a.batch > (int64_t)INT32_MAX * 2) {
         *why = "per-slab extent or band width exceeds the 32-bit addressing of the kernels";
@@ -478,12 +531,18 @@ int launch_circulant_fwd(const CircArgs& a, hipStream_t s, const char** why) {
     p.nqb = 0; p.total_wg = 0;
     p.scale = a.scale;
     p.scale_log2 = a.scale * kLog2e;
-    const bool fast = a.dtype != FA_DTYPE_F32 && a.N % 8 == 0 && circ_aligned16(a.K) && circ_aligned16(a.V) &&
+    const bool fast = (a.dtype == FA_DTYPE_BF16 || a.dtype == FA_DTYPE_F16) && a.N % 8 == 0 && circ_aligned16(a.K) && circ_aligned16(a.V) &&
                       ((a.N + 127) / 128) * a.batch <= INT32_MAX && g_circ_force_generic == 0;
     switch (a.dtype) {
         case FA_DTYPE_BF16: launch_circ_typed<bf16>(p, a.batch, fast, s); break;
         case FA_DTYPE_F16: launch_circ_typed<f16>(p, a.batch, fast, s); break;
         case FA_DTYPE_F32: launch_circ_typed<float>(p, a.batch, false, s); break;
+        case FA_DTYPE_F64: {
+            const int64_t waves = a.N * a.batch;
+            hipLaunchKernelGGL(circ_fwd_f64, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p,
+                               a.scale64 > 0.0 ? a.scale64 : (double)a.scale, a.batch);
+            break;
+        }
         default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
     }
     const hipError_t e = hipGetLastError();

@@ -1132,7 +1132,7 @@ struct SplitPlan {
 static SplitPlan split_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     SplitPlan sp;
     const int Dc = head_dim_class(d), DVc = head_dim_class(dv);
-    if (dtype == FA_DTYPE_F32 || !Dc || !DVc) return sp;
+    if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || !Dc || !DVc) return sp;
     const int64_t rows = (Dc <= 64 && DVc <= 64) ? 512 : 256;
     const int64_t wgs = (N + rows - 1) / rows * batch;
     const int64_t NT = (Nk + kBN - 1) / kBN;
@@ -1246,7 +1246,7 @@ static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 // the generic kernel.
 static bool fwd_pad_fits(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     const int64_t nk8 = (Nk + 7) / 8 * 8;
-    return dtype != FA_DTYPE_F32 && nk8 * d * 2 < INT32_MAX && nk8 * dv * 2 < INT32_MAX &&
+    return dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_F64 && nk8 * d * 2 < INT32_MAX && nk8 * dv * 2 < INT32_MAX &&
            nk8 * (d > dv ? d : dv) * batch < ((int64_t)1 << 40);
 }
 static bool fwd_pad_needed(int dtype, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
@@ -1276,6 +1276,7 @@ __global__ __launch_bounds__(256) void fwd_pad_keys(const T* __restrict__ src, T
 }
 
 int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
+    if (a.dtype == FA_DTYPE_F64) return launch_dense_fwd_f64(a, s, why);
     const int Dc = head_dim_class(a.d), DVc = head_dim_class(a.dv);
     if (!Dc || !DVc) {
         *why = "head dimension exceeds the compiled maximum (128)";

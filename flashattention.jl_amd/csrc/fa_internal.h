@@ -17,6 +17,7 @@ struct DenseArgs {
     float scale;               // already resolved (> 0)
     void* workspace = nullptr; // optional: padded K / V copies for ragged Nk (fa_dense_fwd_workspace)
     size_t workspace_bytes = 0;
+    double scale64 = 0.0;      // Float64 kernels: τ resolved in double (0: use scale)
 };
 
 struct DenseBwdArgs {
@@ -28,6 +29,7 @@ struct DenseBwdArgs {
     float scale;
     void* workspace;
     size_t workspace_bytes;
+    double scale64 = 0.0;      // Float64 kernels: τ resolved in double (0: use scale)
 };
 
 struct WindowGeom {
@@ -50,6 +52,7 @@ struct WindowedArgs {
     float scale;
     void* workspace;
     size_t workspace_bytes;
+    double scale64 = 0.0;
 };
 
 struct WindowedBwdArgs {
@@ -62,6 +65,7 @@ struct WindowedBwdArgs {
     float scale;
     void* workspace;
     size_t workspace_bytes;
+    double scale64 = 0.0;
 };
 
 struct CircArgs {
@@ -71,6 +75,7 @@ struct CircArgs {
     float *l, *m;
     int64_t N, d, dv, batch, W;
     float scale;
+    double scale64 = 0.0;      // Float64 kernel: τ resolved in double (0: use scale)
 };
 
 struct SoftmaxArgs {
@@ -88,6 +93,12 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
 size_t dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why);
+// Float64 (fa_f64.hip): the forward, and the backward's row statistics in double
+// (nD = −rowsum(dO ∘ O), nlse = −(m + ln l)/τ recomputed from Q, K; [batch][N] each)
+int launch_dense_fwd_f64(const DenseArgs& a, hipStream_t s, const char** why);
+int launch_f64_bwd_stats(const DenseBwdArgs& a, double* nD, double* nlse, hipStream_t s, const char** why);
+// element size of a fa_dtype (0: unknown)
+inline size_t dtype_size(int dtype) { return dtype == 0 ? 4 : dtype == 1 || dtype == 2 ? 2 : dtype == 3 ? 8 : 0; }
 size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why);

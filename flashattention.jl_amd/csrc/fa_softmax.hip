@@ -318,6 +318,38 @@ size_t softmax_workspace(int64_t M, int64_t N, int64_t batch, int dims) {
     return (size_t)(nchunk * N * batch) * sizeof(float2) + 256;
 }
 
+// Float64 (the reference's test element type), computed in double.
+// dims = 1: one wave per column, lanes stride the M contiguous elements (three sweeps).
+__global__ __launch_bounds__(256) void sm_cols_f64(const double* __restrict__ S, double* __restrict__ P, int64_t M,
+                                                   int64_t cols) {
+    const int64_t col = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (col >= cols) return;
+    const int lane = threadIdx.x & 63;
+    const double* x = S + col * M;
+    double* y = P + col * M;
+    double m = -__builtin_huge_val(), l = 0.0;
+    for (int64_t i = lane; i < M; i += 64) m = __builtin_elementwise_maximum(m, x[i]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = __builtin_elementwise_maximum(m, __shfl_xor(m, o));
+    for (int64_t i = lane; i < M; i += 64) l += exp(x[i] - m);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) l += __shfl_xor(l, o);
+    const double inv = 1.0 / l;
+    for (int64_t i = lane; i < M; i += 64) y[i] = exp(x[i] - m) * inv;
+}
+// dims = 2: one thread per row (stride M), lanes on consecutive rows (coalesced).
+__global__ __launch_bounds__(256) void sm_rows_f64(const double* __restrict__ S, double* __restrict__ P, int64_t M,
+                                                   int N) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= M) return;
+    const int64_t base = (int64_t)blockIdx.y * M * N + i;
+    double m = -__builtin_huge_val(), l = 0.0;
+    for (int j = 0; j < N; ++j) m = __builtin_elementwise_maximum(m, S[base + (int64_t)j * M]);
+    for (int j = 0; j < N; ++j) l += exp(S[base + (int64_t)j * M] - m);
+    const double inv = 1.0 / l;
+    for (int j = 0; j < N; ++j) P[base + (int64_t)j * M] = exp(S[base + (int64_t)j * M] - m) * inv;
+}
+
 template <class T>
 static void launch_sm_typed(const SoftmaxArgs& a, hipStream_t s) {
     const T* S = (const T*)a.S;
@@ -360,6 +392,16 @@ int launch_softmax(const SoftmaxArgs& a, hipStream_t s, const char** why) {
         case FA_DTYPE_BF16: launch_sm_typed<bf16>(a, s); break;
         case FA_DTYPE_F16: launch_sm_typed<f16>(a, s); break;
         case FA_DTYPE_F32: launch_sm_typed<float>(a, s); break;
+        case FA_DTYPE_F64:
+            if (a.dims == 1) {
+                const int64_t cols = a.N * a.batch;
+                hipLaunchKernelGGL(sm_cols_f64, dim3((unsigned)((cols + 3) / 4)), dim3(256), 0, s, (const double*)a.S,
+                                   (double*)a.P, a.M, cols);
+            } else {
+                hipLaunchKernelGGL(sm_rows_f64, dim3((unsigned)((a.M + 255) / 256), (unsigned)a.batch), dim3(256), 0,
+                                   s, (const double*)a.S, (double*)a.P, a.M, (int)a.N);
+            }
+            break;
         default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
     }
     const hipError_t e = hipGetLastError();

@@ -99,10 +99,11 @@ __global__ __launch_bounds__(256) void win_gather(const T* __restrict__ src, T* 
     const int w = (int)(rest % g.L);
     const int64_t b = rest / g.L;
     const int pix = win_pixel(g, w, t);
-    float v = 0.0f;
+    typedef typename std::conditional<sizeof(T) == 8, double, float>::type A;   // Float64 stays double
+    A v = (A)0;
     if (pix >= 0) {
-        v = (float)src[(b * C + c) * (int64_t)g.P + pix];
-        if constexpr (DIVIDE) v /= (float)win_count(g, pix);
+        v = (A)src[(b * C + c) * (int64_t)g.P + pix];
+        if constexpr (DIVIDE) v /= (A)win_count(g, pix);
     }
     dst[e] = (T)v;
 }
@@ -129,7 +130,8 @@ __global__ __launch_bounds__(256) void win_fold(const T* __restrict__ src, T* __
             hi[i] = min(g.O[i] - 1, (x[i] + g.pad) / g.stride);
         }
     }
-    float acc = 0.0f;
+    typedef typename std::conditional<sizeof(T) == 8, double, float>::type A;   // Float64 stays double
+    A acc = (A)0;
     int cnt = 0;
     for (int o3 = lo[2]; o3 <= hi[2]; ++o3)
         for (int o2 = lo[1]; o2 <= hi[1]; ++o2)
@@ -139,10 +141,10 @@ __global__ __launch_bounds__(256) void win_fold(const T* __restrict__ src, T* __
                 const int t3 = g.nsp > 2 ? x[2] + g.pad - o3 * g.stride : 0;
                 const int w = o1 + g.O[0] * (o2 + g.O[1] * o3);
                 const int t = t1 + g.ws * (t2 + g.ws * t3);
-                acc += (float)src[t + (int64_t)g.T * (c + (int64_t)C * (w + (int64_t)g.L * b))];
+                acc += (A)src[t + (int64_t)g.T * (c + (int64_t)C * (w + (int64_t)g.L * b))];
                 ++cnt;
             }
-    if constexpr (DIVIDE) acc = acc / (float)cnt;   // 0/0 = NaN where uncovered (reference semantics)
+    if constexpr (DIVIDE) acc = acc / (A)cnt;   // 0/0 = NaN where uncovered (reference semantics)
     dst[e] = (T)acc;
 }
 
@@ -1964,7 +1966,7 @@ thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 re
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
 static bool fused_ok(int dtype, const WindowGeom& g, int64_t d, int64_t dv) {
-    return g_win_force_composed != 1 && dtype != FA_DTYPE_F32 && g.T <= 64 && d <= 64 && dv <= 64 &&
+    return g_win_force_composed != 1 && (dtype == FA_DTYPE_BF16 || dtype == FA_DTYPE_F16) && g.T <= 64 && d <= 64 && dv <= 64 &&
            g.P * (d > dv ? d : dv) * 2 < INT32_MAX;
 }
 
@@ -2045,7 +2047,7 @@ static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStr
 // every wave runs two of the four 32-feature output chunks).  The workspace
 // query cannot see the pointers, so it keeps the composed path's size.
 static bool rows128_ok(const WindowedArgs& a) {
-    return g_win_force_composed != 1 && g_win_force_composed != 2 && a.dtype != FA_DTYPE_F32 &&
+    return g_win_force_composed != 1 && g_win_force_composed != 2 && (a.dtype == FA_DTYPE_BF16 || a.dtype == FA_DTYPE_F16) &&
            (a.d > 64 || a.dv > 64) && a.d <= 128 && a.dv <= 128 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
            a.g.ws <= 7 && a.g.S[0] % 8 == 0 && ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 &&
            ((uintptr_t)a.v & 15u) == 0 && a.g.P * 128 * 2 < INT32_MAX &&
@@ -2084,7 +2086,7 @@ static hipError_t launch_fused(const WindowedArgs& a, const WinDev& g, void* out
     return launch_fused_dd<T, 64, 64>(a, g, out, direct, s);
 }
 
-static size_t esize(int dtype) { return dtype == FA_DTYPE_F32 ? 4 : 2; }
+static size_t esize(int dtype) { return dtype_size(dtype); }
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
@@ -2158,7 +2160,7 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
             return FA_OK;
         }
     }
-    if constexpr (!std::is_same<T, float>::value) {
+    if constexpr (sizeof(T) == 2) {
     if (rows128_ok(a)) {
         const int64_t nw = a.g.L * a.batch;
         hipLaunchKernelGGL((win_rows1s<T, 128, 128, 1>), dim3((unsigned)nw), dim3(256), 0, s, (const T*)a.q,
@@ -2211,6 +2213,7 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
     // the window batch has T = ws^k tokens (49 at ws 7): the dense workspace lets
     // the fast kernels run on padded key copies (or split-KV) instead of the generic one
     DenseArgs da{a.dtype, qw, kw, vw, ow, a.l, a.m, a.g.T, a.g.T, a.d, a.dv, a.g.L * a.batch, a.scale};
+    da.scale64 = a.scale64;
     da.workspace = ws;
     da.workspace_bytes = dense_fwd_workspace(a.dtype, a.g.T, a.g.T, a.d, a.dv, a.g.L * a.batch);
     const int rc = launch_dense_fwd(da, s, why);
@@ -2243,6 +2246,8 @@ int launch_window(int dtype, const void* src, void* dst, const WindowGeom& geom,
                                         : gather<f16>(src, dst, (int)C, batch, g, false, s); break;
         case FA_DTYPE_F32: e = unwindow ? fold<float>(src, dst, (int)C, batch, g, false, s)
                                         : gather<float>(src, dst, (int)C, batch, g, false, s); break;
+        case FA_DTYPE_F64: e = unwindow ? fold<double>(src, dst, (int)C, batch, g, false, s)
+                                        : gather<double>(src, dst, (int)C, batch, g, false, s); break;
         default: *why = "unknown dtype"; return FA_ERR_INVALID_ARG;
     }
     if (e != hipSuccess) {
@@ -2265,6 +2270,7 @@ int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why) 
         case FA_DTYPE_BF16: return windowed_fwd_typed<bf16>(a, s, why);
         case FA_DTYPE_F16: return windowed_fwd_typed<f16>(a, s, why);
         case FA_DTYPE_F32: return windowed_fwd_typed<float>(a, s, why);
+        case FA_DTYPE_F64: return windowed_fwd_typed<double>(a, s, why);
     }
     *why = "unknown dtype";
     return FA_ERR_INVALID_ARG;
@@ -2301,12 +2307,14 @@ static int windowed_bwd_typed(const WindowedBwdArgs& a, hipStream_t s, const cha
     }
     // per-window outputs O_w (the backward's D = rowsum(dO_w ∘ O_w) needs them)
     DenseArgs da{a.dtype, qw, kw, vw, ow, lw, mw, a.g.T, a.g.T, a.d, a.dv, nb, a.scale};
+    da.scale64 = a.scale64;
     da.workspace = fwork;
     da.workspace_bytes = fws;
     int rc = launch_dense_fwd(da, s, why);
     if (rc != FA_OK) return rc;
     DenseBwdArgs ba{a.dtype, qw, kw, vw, ow, dyw, a.l, a.m, dqw, dkw, dvw, a.g.T, a.g.T, a.d, a.dv, nb,
                     a.scale, dwork, dws};
+    ba.scale64 = a.scale64;
     rc = launch_dense_bwd(ba, s, why);
     if (rc != FA_OK) return rc;
     if ((e = fold<T>(dqw, a.dq, (int)a.d, a.batch, g, false, s)) != hipSuccess ||
@@ -2322,7 +2330,7 @@ static int windowed_bwd_typed(const WindowedBwdArgs& a, hipStream_t s, const cha
 static bool bwd_rows_ok(const WindowedBwdArgs& a) {
     const bool al = ((uintptr_t)a.q & 15u) == 0 && ((uintptr_t)a.k & 15u) == 0 && ((uintptr_t)a.v & 15u) == 0 &&
                     ((uintptr_t)a.y & 15u) == 0 && ((uintptr_t)a.dy & 15u) == 0;
-    return g_win_force_composed != 1 && a.dtype != FA_DTYPE_F32 && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
+    return g_win_force_composed != 1 && (a.dtype == FA_DTYPE_BF16 || a.dtype == FA_DTYPE_F16) && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
            a.g.ws <= 7 && a.g.S[0] % 8 == 0 && a.d <= 128 && a.dv <= 128 && al &&
            a.g.P * 128 * 2 < INT32_MAX;
 }
@@ -2413,6 +2421,7 @@ int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** wh
         case FA_DTYPE_BF16: return windowed_bwd_typed<bf16>(a, s, why);
         case FA_DTYPE_F16: return windowed_bwd_typed<f16>(a, s, why);
         case FA_DTYPE_F32: return windowed_bwd_typed<float>(a, s, why);
+        case FA_DTYPE_F64: return windowed_bwd_typed<double>(a, s, why);
     }
     *why = "unknown dtype";
     return FA_ERR_INVALID_ARG;

@@ -59,7 +59,7 @@ class FlashAttentionError(RuntimeError):
 
 
 FA_OK, FA_ERR_INVALID_ARG, FA_ERR_UNSUPPORTED, FA_ERR_HIP, FA_ERR_WORKSPACE = range(5)
-DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
 
 # ----------------------------------------------------------------------------
 # library loading (the C ABI is the only compute path)
@@ -211,7 +211,7 @@ def _dtype_code(*ts: torch.Tensor) -> int:
     for t in ts:
         _require(t.dtype == dt, f"mixed element types {dt} and {t.dtype}")
     if dt not in DTYPES:
-        raise TypeError(f"unsupported element type {dt}; use float32, bfloat16 or float16")
+        raise TypeError(f"unsupported element type {dt}; use float64, float32, bfloat16 or float16")
     return DTYPES[dt]
 
 
@@ -250,7 +250,7 @@ def dense_fa_(O: torch.Tensor, l: torch.Tensor, m: torch.Tensor,
     _device_check(Q, K, V, O, l, m)
     Lb = lib()
     nws = Lb.fa_dense_fwd_workspace(code, N, Nk, d, dv, B) if hasattr(Lb, "fa_dense_fwd_ws") else 0
-    if (code != DTYPES[torch.float32] and N * Nk * B > 0 and Nk % 8 == 0
+    if (code in (DTYPES[torch.bfloat16], DTYPES[torch.float16]) and N * Nk * B > 0 and Nk % 8 == 0
             and (K.data_ptr() % 16 or V.data_ptr() % 16)):
         # K / V not 16-B aligned (a view at an odd offset): add room for the
         # padded K / V copies the fast kernels then run on (fa_fwd.hip

@@ -20,10 +20,10 @@
 
 const libfa_hip = get(ENV, "FA_HIP_LIB", joinpath(@__DIR__, "..", "libfa_hip.so"))
 
-const FA_DTYPE = Dict(Float32 => Cint(0), AMDGPU.BFloat16 => Cint(1), Float16 => Cint(2))
+const FA_DTYPE = Dict(Float32 => Cint(0), AMDGPU.BFloat16 => Cint(1), Float16 => Cint(2), Float64 => Cint(3))
 
 fa_dtype(::Type{T}) where {T} = haskey(FA_DTYPE, T) ? FA_DTYPE[T] :
-    throw(ArgumentError("FlashAttentionHIP: element type $T not supported (Float32, Float16, BFloat16)"))
+    throw(ArgumentError("FlashAttentionHIP: element type $T not supported (Float64, Float32, Float16, BFloat16)"))
 
 function fa_check(rc::Cint)
     rc == 0 && return nothing

@@ -35,12 +35,17 @@ extern "C" {
 #define FA_HIP_ABI_VERSION 1
 
 /* Element type of Q, K, V, O (and dO, dQ, dK, dV).  l, m are always float32
- * (documented deviation for 16-bit types: the reference keeps them in T,
- * src/dense.jl:12-13). */
+ * (documented deviation: the reference keeps them in T, src/dense.jl:12-13).
+ * FA_DTYPE_F64 is the element type of the reference's own tests and timings
+ * (test/test.jl:12, logs/compare1.txt): dense forward / backward, the windowed
+ * forward / backward, window / unwindow, circulant and softmax accept it; it runs
+ * fp64 SIMT parity kernels, and its backward recomputes the row statistics in
+ * double instead of reading the float32 l, m. */
 typedef enum fa_dtype {
     FA_DTYPE_F32  = 0,
     FA_DTYPE_BF16 = 1,
-    FA_DTYPE_F16  = 2
+    FA_DTYPE_F16  = 2,
+    FA_DTYPE_F64  = 3
 } fa_dtype;
 
 typedef enum fa_status {
