@@ -30,6 +30,19 @@ using Test, NNlib, AMDGPU, FlashAttention
     end
 end
 
+# test/test.jl exactly as the reference runs it: Float64 arrays, Float64 `≈`
+@testset "HIP dense_fa ≈ CPU dense_dpa in Float64 (test/test.jl:5-21)" begin
+    q, k, v = rand(30, 12, 2), rand(30, 12, 2), rand(30, 6, 2)
+    y1, _ = dense_dpa(q, k, v)
+    yd, _, _ = dense_fa(ROCArray(q), ROCArray(k), ROCArray(v))
+    @test Array(yd) ≈ y1
+    Q, K, V, dO = (ROCArray(rand(64, 32, 2)) for _ in 1:4)
+    O, l, m = dense_fa(Q, K, V)
+    dQ, dK, dV = dense_fa_backward(Q, K, V, O, dO, l, m)
+    @test eltype(dQ) == Float64
+    @test isapprox(vec(sum(Array(dK); dims=1)), zeros(64); atol=1e-10)   # Σ_keys dK = 0
+end
+
 @testset "HIP windowed_fa / block_fa vs CPU windowed_dpa" begin
     x = rand(Float32, 16, 16, 8, 2)
     yc, _ = windowed_dpa(x, x, x, 4; stride=4, pad=0)
