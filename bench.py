@@ -29,8 +29,9 @@ Secondary blocks on the same JSON line (never the headline `value`):
     all ranks' FLOPs / the slowest rank's time.
   * "cpu_baseline" (rank 0, N = 1): the reference's CPU algorithm
     (oracle/fa_cpu.c BLAS port of dense_fa!) on configs[0] at 1 thread and at
-    the process's cores (median of 50 after 5 warm-ups), and on the whole
-    configs[1] workload (fp32).
+    the process's cores (median of 50 after 5 warm-ups), the reference's own
+    published Float64 case (512, 64, 1) likewise, and the whole configs[1]
+    workload (fp32).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-cfg5] [--extra]
 Multi-GPU: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
@@ -74,7 +75,9 @@ def dist_init(backend: str | None = None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # FA_BENCH_BACKEND=gloo rehearses the multi-rank path on a one-GPU box
+        # (every rank on cuda:0; RCCL refuses two ranks on one GPU)
+        backend = os.environ.get("FA_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     if world > 1:
@@ -298,6 +301,14 @@ def cpu_baseline():
     for th in sorted({1, threads}):
         t = med_time(lambda: cpu_port.dense_fa_blas(q0, k0, v0, th), 50, 5)
         c0[f"threads_{th}"] = {"ms": t * 1e3, "gflops": f0 / t / 1e9}
+    # the reference's own published case, as it ran it: Float64, (N, d, bs) = (512, 64, 1)
+    # (logs/compare1.txt:4: 2.392 ms), 1 thread and all usable cores
+    qr, kr, vr = (np.asfortranarray(rng.standard_normal((512, 64, 1))) for _ in range(3))
+    fr = 4.0 * 512 * 512 * 64
+    cr = {}
+    for th in sorted({1, threads}):
+        t = med_time(lambda: cpu_port.dense_fa_blas(qr, kr, vr, th), 50, 5)
+        cr[f"threads_{th}"] = {"ms": t * 1e3, "gflops": fr / t / 1e9}
     q1, k1, v1 = arrs(N_, D_, B_ * H_)
     t1 = med_time(lambda: cpu_port.dense_fa_blas(q1, k1, v1, threads), 3, 1)
     f1 = 4.0 * B_ * H_ * N_ * N_ * D_
@@ -308,6 +319,7 @@ def cpu_baseline():
                       f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles, OpenBLAS sgemm per tile product, {threads} threads), "
                       f"median of 3: {t1:.2f} s",
             "configs0_fp32_512x64x4": c0,
+            "reference_case_f64_512x64x1": cr,
             "reference_published": "dense_fa Julia N=512 d=64 bs=1 Float64: 2.392 ms, unstated CPU "
                                    "(/root/reference/logs/compare1.txt:4)"}
 
