@@ -498,3 +498,41 @@ def test_empty_batch_other_entries(fa):
     P = fa.fused_softmax(S, dims=1)
     torch.cuda.synchronize()
     assert tuple(P.shape) == (8, 8, 0)
+
+
+# Tight error budget for the 16-bit forward, beyond the generic 2e-2·(1+|y|)
+# envelope of conftest.TOL: the output is rounded to T once (half an ulp: 2^-9
+# relative for bf16, 2^-12 for fp16) and P is quantised to T before the PV
+# product (the lazy rescale lets P reach 2^8 first), so every element
+# must sit within a few output ulps of the float64 oracle on the same
+# T-representable inputs, and the mean error far below one ulp.
+BUDGET = {"bfloat16": (4e-3, 2e-3, 1.5e-3), "float16": (1e-3, 4e-4, 2e-4)}   # rel, abs, mean rel
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("case", ["golden", "cfg1_slabs"])
+def test_forward_16bit_error_budget(fa, dtype, case):
+    rel, ab, mean = BUDGET[dtype]
+    cases = []
+    if case == "golden":
+        for path in golden_files("dense_"):
+            g = load_golden(path)
+            cases.append((g["q"], g["k"], g["v"], g["y"].astype(np.float64)))
+    else:   # two slabs of configs[1]'s shape, randn inputs rounded to T
+        rng = np.random.default_rng(99)
+        rt = lambda a: torch.tensor(a).to(DT[dtype]).double().numpy()
+        q, k, v = (rt(rng.standard_normal((4096, 64, 2))) for _ in range(3))
+        cases.append((q, k, v, O.dense_fa3(q, k, v)[0]))
+    worst = worst_mean = 0.0
+    for q, k, v, yr in cases:
+        y, _, _ = fa.dense_fa(*(fa.jl_tensor(a, DT[dtype]) for a in (q, k, v)))
+        torch.cuda.synchronize()
+        yg = _np(y).reshape(yr.shape)
+        err = np.abs(yg - yr)
+        ratio = (err / (rel * np.abs(yr) + ab)).max()
+        worst = max(worst, ratio)
+        assert ratio <= 1.0, f"{dtype}: max err {err.max():.3e} beyond {rel}·|y| + {ab} (ratio {ratio:.2f})"
+        mlim = mean * np.abs(yr).mean() + ab / 20
+        assert err.mean() <= mlim, f"{dtype}: mean err {err.mean():.3e} > {mlim:.3e}"
+        worst_mean = max(worst_mean, err.mean() / mlim)
+    print(f"{dtype} {case}: worst max err / budget = {worst:.3f}, worst mean err / budget = {worst_mean:.3f}")
