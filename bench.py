@@ -498,6 +498,14 @@ def extra_benches(fa_hip, args, dist):
         t = time_graph(lambda: fa_hip.dense_fa_(Of, lf, mf, Qf, Kf, Vf), args.steps, dist)
         res[f"f64_dense_N{Nf}_d64_B{Bf}_us"] = t * 1e6
         res[f"f64_dense_N{Nf}_d64_B{Bf}_gflops"] = 4.0 * Bf * Nf * Nf * 64 / t / 1e9
+    # the reference's runwindow benchmark (bench/compare.jl:105-115: 1-D windowed_fa,
+    # N = 4096, d = 32, bs = 1, stride 8, pad 0, Float64; logs/wind_t16.txt at 16
+    # threads: W = 16 / 128 / 512 -> 10.4 / 115.1 / 805.0 ms), in Float64 and bf16
+    for Ww in (16, 128, 512):
+        for dt, tag in ((torch.float64, "f64"), (torch.bfloat16, "bf16")):
+            qw, kw, vw = (_randn_jl(fa_hip, (4096, 32, 1), dt, gen) for _ in range(3))
+            t = time_graph(lambda: fa_hip.windowed_fa(qw, kw, vw, Ww, stride=8, pad=0), max(5, args.steps // 4), dist)
+            res[f"runwindow_W{Ww}_{tag}_us"] = t * 1e6
     # fused softmax: a configs[1]-shaped score tensor
     # (4096 x 4096 x 64 bf16, 2 GiB) along each dim; HBM-bound: read + write
     Ssm = _randn_jl(fa_hip, (4096, 4096, 64), torch.bfloat16, gen)

@@ -317,3 +317,20 @@ def test_softmax_f64_special_values(fa):
     torch.cuda.synchronize()
     assert np.all(np.isnan(P[:, 0])) and np.all(np.isnan(P[:, 1]))
     close64(P[:, 2], np.full(4, 0.25), "uniform column")
+
+
+@pytest.mark.parametrize("W", [16, 128])
+def test_reference_runwindow_case_f64(fa, W):
+    """bench/compare.jl:32-57 / :105-115 (runwindow: N = 4096, d = 32, bs = 1,
+    stride 8, pad 0, Float64): the reference asserts windowed_dpa ≈ windowed_fa
+    at its own benchmark shape; here the device windowed_fa against the oracle and
+    against the device's materialising windowed_dpa, at Float64 `≈`."""
+    rng = np.random.default_rng(W)
+    q, k, v = (rng.standard_normal((4096, 32, 1)) for _ in range(3))
+    Q, K, V = (fa.jl_tensor(a, F64) for a in (q, k, v))
+    y, l, m = fa.windowed_fa(Q, K, V, W, stride=8, pad=0)
+    yd, _ = fa.windowed_dpa(Q, K, V, W, 8, 0)
+    yr, _, _ = O.windowed_fa(q, k, v, W, 8, 0)
+    torch.cuda.synchronize()
+    close64(_np(y), yr, "windowed_fa vs oracle", nan_ok=True)
+    close64(_np(yd), _np(y), "windowed_dpa vs windowed_fa", nan_ok=True)
