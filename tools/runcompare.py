@@ -16,6 +16,9 @@ Julia's `≈` at the element type (Float64 rows).  The reference's published
 seconds (Julia Float64 on the CPU, unstated machine) are copied below as data
 from logs/compare1.txt:3-9 and printed beside ours.
 
+Also runcirculant (logs/circ_t16.txt) in Float64 and run_col_softmax
+(logs/sm_cuda.txt, the reference's CUDA fused softmax) in Float32.
+
     python tools/runcompare.py [--dtype f64|bf16|both] > gpurun_out/runcompare.log
 """
 from __future__ import annotations
@@ -45,6 +48,19 @@ REFERENCE = {
     8192: (0.844029, 0.092271, 0.036167, 0.033633, 0.148966, 0.136042, 0.232847, 0.055418),
     16384: (3.367637, 0.348872, 0.091136, 0.084757, 0.269094, 0.244971, 0.463745, 0.101374),
 }
+# logs/circ_t16.txt:3-9 (runcirculant, N 4096, d 32, bs 1, Float64, 16 threads):
+# W -> (circ_dpa, circ_fa) seconds
+REFERENCE_CIRC = {16: (0.021980, 0.004450), 32: (0.044041, 0.007519), 64: (0.087498, 0.015007),
+                  128: (0.175385, 0.027255), 256: (0.362050, 0.058335), 512: (0.741904, 0.133951),
+                  1024: (1.549231, 0.282095)}
+# logs/sm_cuda.txt:2-14 (run_col_softmax, bench/softmax.jl:36-57: Float32 (M, N), dims 1,
+# on the reference's CUDA GPU): (M, N) -> (naive, fused, nnlib) seconds
+REFERENCE_SM = {(256, 65536): (0.001491, 0.001329, 0.000225), (512, 65536): (0.003097, 0.001456, 0.000405),
+                (1024, 65536): (0.004624, 0.001843, 0.000789), (2048, 65536): (0.007390, 0.002893, 0.002418),
+                (4096, 65536): (0.013122, 0.004958, 0.006674), (8192, 65536): (0.026448, 0.008687, 0.013952),
+                (256, 131072): (0.011195, 0.002552, 0.000411), (512, 131072): (0.023322, 0.002800, 0.000754),
+                (1024, 131072): (0.044907, 0.003602, 0.001662), (2048, 131072): (0.090770, 0.005609, 0.004767),
+                (4096, 131072): (0.176741, 0.009624, 0.013177), (8192, 131072): (0.377765, 0.016920, 0.027901)}
 COLS = ("dense_dpa", "dense_fa", "block_dpa", "block_fa", "wind_dpa", "wind_fa", "circ_dpa", "circ_fa")
 WS = 64
 
@@ -96,6 +112,39 @@ def run(dt, steps):
     return rows
 
 
+def run_circulant(steps):
+    """runcirculant (bench/compare.jl:118-130) in Float64, timed beside
+    logs/circ_t16.txt (its parity is tests/test_gpu_float64.py::test_circulant_*)."""
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    Q, K, V = (bench._randn_jl(fa_hip, (4096, 32, 1), torch.float64, gen) for _ in range(3))
+    rows = []
+    for W, (rdpa, rfa) in sorted(REFERENCE_CIRC.items()):
+        t = timed(lambda: fa_hip.circulant_fa(Q, K, V, W), steps)
+        rows.append({"W": W, "circ_fa_s": t, "reference_circ_fa_s": rfa, "speedup": rfa / t})
+        print(f"circ W={W:5d}: {t * 1e3:8.4f} ms (ref {rfa * 1e3:8.3f} ms)", flush=True)
+    return rows
+
+
+def run_softmax(steps):
+    """run_col_softmax (bench/softmax.jl:36-78): Float32 column softmax of (M, N),
+    with the reference's own check fused ≈ NNlib.softmax (torch.softmax here)."""
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    rows = []
+    for (M, N), (rn, rf, rl) in sorted(REFERENCE_SM.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+        S = fa_hip.jl_empty((M, N, 1), torch.float32)
+        S.uniform_(generator=gen)
+        P = torch.empty_like(S)
+        t = timed(lambda: fa_hip.fused_softmax_(P, S, 1), steps)
+        fa_hip.fused_softmax_(P, S, 1)
+        ref = torch.softmax(S.permute(2, 1, 0), dim=-1).permute(2, 1, 0)   # over M (dims = 1)
+        ok = approx(P, ref, torch.float32)
+        rows.append({"M": M, "N": N, "fused_s": t, "reference_fused_s": rf, "reference_nnlib_s": rl,
+                     "speedup_vs_fused": rf / t, "approx_nnlib": ok})
+        print(f"softmax M={M:5d} N={N:6d}: {t * 1e3:8.4f} ms (ref CUDA fused {rf * 1e3:7.3f}, NNlib {rl * 1e3:7.3f}) ≈ {ok}",
+              flush=True)
+    return rows
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="both", choices=["f64", "bf16", "both"])
@@ -106,7 +155,10 @@ def main():
     for dt in dts:
         print(f"# {dt}: N d=64 bs=1 | " + " ".join(f"{c:>9s}" for c in COLS if c != "circ_dpa"), flush=True)
         out[str(dt)] = run(dt, a.steps)
-    print(json.dumps({"runcompare": out, "reference": "logs/compare1.txt:3-9 (Julia Float64, CPU)"}))
+    circ = run_circulant(a.steps)
+    sm = run_softmax(a.steps)
+    print(json.dumps({"runcompare": out, "reference": "logs/compare1.txt:3-9 (Julia Float64, CPU)",
+                      "runcirculant_f64": circ, "run_col_softmax_f32": sm}))
 
 
 if __name__ == "__main__":
