@@ -38,7 +38,7 @@ __all__ = [
     "DimensionMismatch", "FlashAttentionError", "lib", "lib_path",
     "jl_empty", "jl_zeros", "jl_tensor", "jl_strides", "is_jl_contiguous",
     "dense_fa", "dense_fa_", "dense_fa_backward", "windowed_fa", "block_fa",
-    "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_",
+    "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_", "circulant_dpa",
     "fused_softmax", "fused_softmax_", "DTYPES",
 ]
 
@@ -571,6 +571,55 @@ def windowed_dpa(q, k, v, windowsize: int, stride: Optional[int] = None, pad: Op
     y = unwindow(jl_reshape(yw, (T, dvo, L, B)), szy, windowsize, stride, pad)
     y.div_(divisor)
     return y, jl_reshape(Pw, (T, T, L, B))
+
+
+def circulant_band_index(N: int, W: int, device="cuda") -> torch.Tensor:
+    """0-based key index J[w, i] of band entry w of query i, in the reference's
+    order: ``cartesian_circulant((i-1)*W + w, N, W)[1]`` (src/utils.jl:6-17, used
+    by src/naive/circulant.jl:21-22 and src/circulant.jl:74-75), vectorised.
+    The keys of query i are (i − p + t) mod N, t < W, p = (W−1)÷2; the reference's
+    circshift only rotates their order for the first and last p columns."""
+    p = (W - 1) // 2
+    i = torch.arange(N, device=device, dtype=torch.int64)[None, :]
+    w = torch.arange(W, device=device, dtype=torch.int64)[:, None]
+    j1 = i + 1                                            # 1-based column
+    m0 = torch.where(j1 <= p, torch.remainder(w - i + p, W),
+                     torch.where(j1 > N - p, torch.remainder(w - p + N - i - 1, W), w.expand(W, N)))
+    return torch.remainder(m0 + i - p, N)
+
+
+def circulant_dpa(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, W: int, scale: float = 0.0):
+    """``circulant_dpa(Q, K, V, W) -> (O, P)`` — src/naive/circulant.jl:1-36, the
+    reference's materialising banded attention (its check for circulant_fa,
+    bench/compare.jl:72-74): band scores P[w, i, b] = τ qᵢ·k_J[w,i] (:19-24),
+    softmax over the band (dims = 1, this library's fa_softmax kernel, :27),
+    O = Σ_w P[w, i] v_J[w,i] (:28-34).
+
+    Representation deviation: the reference returns P as the transposed sparse
+    circulant matrix (``batch_circulant(P) |> transpose``, :28); this returns its
+    nonzeros, the (W, N, B) band array the reference builds it from, in the same
+    entry order.  Gathers and reductions are torch ops on the device; memory is
+    O(W·N·d·B)."""
+    _require(Q.dim() == 3 and K.dim() == 3 and V.dim() == 3, "circulant_dpa expects 3-D (N, d, batch) arrays")
+    N, d, B = Q.shape
+    dv = V.shape[1]
+    _require(K.shape == (N, d, B) and V.shape == (N, dv, B), "DimensionMismatch: K must match Q, V (N, dv, batch)")
+    _require(int(W) >= 1, "DimensionMismatch: window size W must be >= 1")
+    _dtype_code(Q, K, V)
+    _device_check(Q, K, V)
+    W = int(W)
+    tau = float(scale) if scale > 0 else 1.0 / math.sqrt(d)
+    J = circulant_band_index(N, W, Q.device)              # (W, N)
+    Qr, Kr, Vr = _rm(Q), _rm(K), _rm(V)                   # [B][d][N], [B][d][N], [B][dv][N]
+    acc = torch.float64 if Q.dtype == torch.float64 else torch.float32
+    S = (Kr[:, :, J].to(acc) * Qr[:, :, None, :].to(acc)).sum(1) * tau    # [B][W][N]
+    P = jl_empty((W, N, B), Q.dtype, Q.device)
+    _rm(P).copy_(S.transpose(1, 2))                       # column-major (W, N, B) = [B][N][W]
+    fused_softmax_(P, P, dims=1)
+    Pw = _rm(P).transpose(1, 2).to(acc)                   # [B][W][N]
+    O = jl_empty((N, dv, B), Q.dtype, Q.device)
+    _rm(O).copy_((Vr[:, :, J].to(acc) * Pw[:, None, :, :]).sum(2))   # [B][dv][N]
+    return O, P
 
 
 def block_dpa(q, k, v, windowsize: int):

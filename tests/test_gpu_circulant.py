@@ -156,3 +156,23 @@ def test_circulant_simt_vs_reference_kernel(fa, N, d, dv, W, dtype):
     assert_lm_close(_np(l1), lr, dtype, "l")
     assert_lm_close(_np(m1), mr, dtype, "m")
     assert_close(_np(o1), _np(o2), dtype, "O simt vs one-wave")
+
+
+@pytest.mark.parametrize("dtype", list(DT))
+@pytest.mark.parametrize("N,d,dv,W,B", [(96, 32, 16, 7, 2), (200, 64, 64, 65, 1), (50, 16, 8, 64, 2)])
+def test_circulant_dpa_vs_oracle(fa, dtype, N, d, dv, W, B):
+    """circulant_dpa (src/naive/circulant.jl:1-36): O and the (W, N, B) band P vs
+    the oracle, and the reference's own check circulant_dpa ≈ circulant_fa
+    (bench/compare.jl:72-74)."""
+    rng = np.random.default_rng(N + W)
+    rt = lambda a: torch.tensor(a).to(DT[dtype]).double().numpy()
+    q, k, v = rt(rng.standard_normal((N, d, B))), rt(rng.standard_normal((N, d, B))), rt(rng.standard_normal((N, dv, B)))
+    Q, K, V = (fa.jl_tensor(a, DT[dtype]) for a in (q, k, v))
+    o, P = fa.circulant_dpa(Q, K, V, W)
+    of, _, _ = fa.circulant_fa(Q, K, V, W)
+    orf, Pr = O.circulant_dpa3(q, k, v, W)
+    torch.cuda.synchronize()
+    assert tuple(P.shape) == (W, N, B) and fa.is_jl_contiguous(P)
+    assert_close(_np(o), orf, dtype, "O")
+    assert_close(_np(P), Pr, dtype, "P")
+    assert_close(_np(o), _np(of), dtype, "circulant_dpa vs circulant_fa")

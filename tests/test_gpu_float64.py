@@ -334,3 +334,19 @@ def test_reference_runwindow_case_f64(fa, W):
     torch.cuda.synchronize()
     close64(_np(y), yr, "windowed_fa vs oracle", nan_ok=True)
     close64(_np(yd), _np(y), "windowed_dpa vs windowed_fa", nan_ok=True)
+
+
+@pytest.mark.parametrize("N,W", [(4096, 16), (4096, 129), (300, 301)])
+def test_circulant_dpa_f64(fa, N, W):
+    """circulant_dpa ≈ circulant_fa at Float64 (bench/compare.jl:72-74, the
+    reference's runcirculant shape N = 4096, d = 32) and both vs the oracle."""
+    rng = np.random.default_rng(W)
+    q, k, v = (rng.standard_normal((N, 32, 1)) for _ in range(3))
+    Q, K, V = (fa.jl_tensor(a, F64) for a in (q, k, v))
+    o, P = fa.circulant_dpa(Q, K, V, W)
+    of, _, _ = fa.circulant_fa(Q, K, V, W)
+    orf, Pr = O.circulant_dpa3(q, k, v, W)
+    torch.cuda.synchronize()
+    close64(_np(o), orf, "O")
+    close64(_np(P), Pr, "P")
+    close64(_np(of), _np(o), "circulant_fa vs circulant_dpa")

@@ -76,3 +76,14 @@ def test_valid_windowed_backward_shapes_reach_the_device_check():
     q, k, v, y, dy, l, m = _win_inputs()
     with pytest.raises(TypeError, match="ROCm device"):
         fa_hip.windowed_fa_backward(q, k, v, y, dy, l, m, 7)
+
+
+def test_circulant_band_index_matches_oracle():
+    """fa_hip.circulant_band_index (vectorised, used by circulant_dpa) equals the
+    oracle's loop over the reference's cartesian_circulant (src/utils.jl:6-17),
+    including even W, W = 1 and W > N."""
+    import numpy as np
+    from oracle import fa_oracle as O
+    for N, W in [(10, 3), (17, 5), (9, 4), (8, 11), (30, 1), (64, 65), (5, 5), (100, 16)]:
+        J = fa_hip.circulant_band_index(N, W, "cpu").numpy()
+        assert np.array_equal(J, O.circulant_index(N, W)), (N, W)

@@ -8,7 +8,7 @@ logs/compare1.txt) through this library, in Float64 as the reference ran it
   dense_dpa / dense_fa            (N, 64, 1)
   block_dpa / block_fa            windowsize 64, stride 64, pad 0
   wind_dpa  / wind_fa             windowsize 64, stride 16, pad 0
-  circ_fa                         W = windowsize + 1 = 65
+  circ_dpa  / circ_fa             W = windowsize + 1 = 65
 
 Every row also repeats the reference's own check (`@test O1 ≈ O2`,
 bench/compare.jl:20,47,74): the device's materialising *_dpa against its *_fa,
@@ -100,7 +100,9 @@ def run(dt, steps):
         t["wind_fa"] = timed(lambda: fa_hip.windowed_fa(Q, K, V, WS, stride=16, pad=0), steps)
         ok["wind"] = approx(fa_hip.windowed_dpa(Q, K, V, WS, 16, 0)[0],
                             fa_hip.windowed_fa(Q, K, V, WS, stride=16, pad=0)[0], dt)
+        t["circ_dpa"] = timed(lambda: fa_hip.circulant_dpa(Q, K, V, WS + 1), steps)
         t["circ_fa"] = timed(lambda: fa_hip.circulant_fa(Q, K, V, WS + 1), steps)
+        ok["circ"] = approx(fa_hip.circulant_dpa(Q, K, V, WS + 1)[0], fa_hip.circulant_fa(Q, K, V, WS + 1)[0], dt)
         torch.cuda.synchronize()
         ref = dict(zip(COLS, REFERENCE[N]))
         rows.append({"N": N, "d": 64, "bs": 1, "dtype": str(dt).replace("torch.", ""),
@@ -153,7 +155,7 @@ def main():
     dts = {"f64": [torch.float64], "bf16": [torch.bfloat16], "both": [torch.float64, torch.bfloat16]}[a.dtype]
     out = {}
     for dt in dts:
-        print(f"# {dt}: N d=64 bs=1 | " + " ".join(f"{c:>9s}" for c in COLS if c != "circ_dpa"), flush=True)
+        print(f"# {dt}: N d=64 bs=1 | " + " ".join(f"{c:>9s}" for c in COLS), flush=True)
         out[str(dt)] = run(dt, a.steps)
     circ = run_circulant(a.steps)
     sm = run_softmax(a.steps)
