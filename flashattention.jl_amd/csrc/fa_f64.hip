@@ -9,12 +9,14 @@
 // algorithm (src/dense.jl:21-102) with the FA-2 deferred normalisation of the
 // other kernels:
 //
-//  * one workgroup = 256 threads = 64 queries of one slab; Q stays in LDS as a
-//    [feature][64] image (coalesced loads along tokens, conflict-free reads);
-//  * keys stream in tiles of 32 ([feature][32] images, rows read as broadcasts);
-//  * thread (qi, g) scores keys 8g .. 8g+7 of the tile for query qi, the row max
-//    and row sum go through a [4][64] LDS exchange, and the same thread then owns
-//    output channels g, g+4, … of query qi (the O rescale needs no exchange);
+//  * one workgroup = 256 threads = QB = 64 queries of one slab (16 when 64 would
+//    leave CUs idle: 4x the workgroups); Q stays in LDS as a [feature][QB] image
+//    (coalesced loads along tokens);
+//  * keys stream in tiles of 32 ([feature][32] images);
+//  * thread (qi, g), g < NG = 256/QB, scores keys KPG·g .. KPG·g + KPG − 1 of the
+//    tile for query qi, the row max and row sum go through an [NG][QB] LDS
+//    exchange, and the same thread then owns output channels g, g + NG, … of query
+//    qi (the O rescale needs no exchange);
 //  * exp / log in double; τ is resolved in double (1/√d, src/dense.jl:43).
 //
 // l and m leave as float32 (the C ABI's type for every dtype).  The backward does
@@ -37,40 +39,43 @@ struct F64Params {
     double scale;
 };
 
-constexpr int kQB64 = 64;    // queries per workgroup
+constexpr int kQB64 = 64;    // queries per workgroup (QB = 16 for grids smaller than the chip)
 constexpr int kKB64 = 32;    // keys per tile
 constexpr int kTh64 = 256;
-constexpr int kOPer64 = kMaxHeadDim / 4;   // output channels per thread
 
 __device__ __forceinline__ double dmax(double a, double b) { return __builtin_elementwise_maximum(a, b); }
 
-static size_t f64_lds_bytes(int d, int dv, bool stats) {
-    return sizeof(double) * ((size_t)kQB64 * d + (size_t)kKB64 * d + (stats ? 0 : (size_t)kKB64 * dv) +
-                             (stats ? 0 : (size_t)kQB64 * (kKB64 + 1)) + 2 * 4 * kQB64);
+static size_t f64_lds_bytes(int d, int dv, bool stats, int QB) {
+    return sizeof(double) * ((size_t)QB * d + (size_t)kKB64 * d + (stats ? 0 : (size_t)kKB64 * dv) +
+                             (stats ? 0 : (size_t)QB * (kKB64 + 1)) + 2 * kTh64);
 }
 
-template <bool STATS>
+// QB queries per workgroup, NG = 256/QB thread groups per query: group g scores
+// keys KPG·g .. KPG·g + KPG−1 of each tile and owns output channels g, g + NG, ….
+template <bool STATS, int QB>
 __global__ __launch_bounds__(kTh64) void dense_fwd_f64(F64Params p) {
+    constexpr int NG = kTh64 / QB, KPG = kKB64 / NG, OPER = kMaxHeadDim / NG;
+    static_assert(KPG >= 1 && QB * NG == kTh64, "geometry");
     extern __shared__ __attribute__((aligned(16))) double sm64[];
     const int d = p.d, dv = p.dv, N = p.N, Nk = p.Nk;
-    double* const sQ = sm64;                                    // [d][64]
-    double* const sK = sQ + kQB64 * d;                          // [d][32]
+    double* const sQ = sm64;                                    // [d][QB]
+    double* const sK = sQ + QB * d;                             // [d][32]
     double* const sV = sK + kKB64 * d;                          // [dv][32]
-    double* const sP = sV + (STATS ? 0 : kKB64 * dv);           // [64][33]
-    double* const red = sP + (STATS ? 0 : kQB64 * (kKB64 + 1)); // [2][4][64]: tile max, tile sum
-    const int b = blockIdx.x / p.nqb, q0 = (blockIdx.x - b * p.nqb) * kQB64;
-    const int tid = threadIdx.x, qi = tid & 63, g = tid >> 6;
+    double* const sP = sV + (STATS ? 0 : kKB64 * dv);           // [QB][33]
+    double* const red = sP + (STATS ? 0 : QB * (kKB64 + 1));    // [2][NG][QB]: tile max, tile sum
+    const int b = blockIdx.x / p.nqb, q0 = (blockIdx.x - b * p.nqb) * QB;
+    const int tid = threadIdx.x, qi = tid % QB, g = tid / QB;
     const double* __restrict__ Qb = p.Q + (int64_t)b * N * d;
     const double* __restrict__ Kb = p.K + (int64_t)b * Nk * d;
     const double* __restrict__ Vb = STATS ? nullptr : p.V + (int64_t)b * Nk * dv;
 
-    for (int i = tid; i < kQB64 * d; i += kTh64) {
-        const int f = i >> 6, q = i & 63;
+    for (int i = tid; i < QB * d; i += kTh64) {
+        const int f = i / QB, q = i % QB;
         sQ[i] = q0 + q < N ? Qb[(int64_t)f * N + q0 + q] : 0.0;
     }
-    double o[kOPer64];
+    double o[OPER];
 #pragma unroll
-    for (int i = 0; i < kOPer64; ++i) o[i] = 0.0;
+    for (int i = 0; i < OPER; ++i) o[i] = 0.0;
     double m_run = -__builtin_huge_val(), l_run = 0.0;
 
     for (int k0 = 0; k0 < Nk; k0 += kKB64) {
@@ -86,47 +91,51 @@ __global__ __launch_bounds__(kTh64) void dense_fwd_f64(F64Params p) {
             }
         __syncthreads();
 
-        // scores of keys 8g .. 8g+7 for query qi (s = τ qᵀk, src/dense.jl:77)
-        double s[8];
+        // scores of keys KPG·g .. KPG·g + KPG−1 for query qi (s = τ qᵀk, src/dense.jl:77)
+        double s[KPG];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] = 0.0;
+        for (int j = 0; j < KPG; ++j) s[j] = 0.0;
         for (int f = 0; f < d; ++f) {
-            const double qv = sQ[f * kQB64 + qi];
-            const double* kr = sK + f * kKB64 + 8 * g;
+            const double qv = sQ[f * QB + qi];
+            const double* kr = sK + f * kKB64 + KPG * g;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) s[j] = fma(qv, kr[j], s[j]);
+            for (int j = 0; j < KPG; ++j) s[j] = fma(qv, kr[j], s[j]);
         }
         double mx = -__builtin_huge_val();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            s[j] = k0 + 8 * g + j < Nk ? s[j] * p.scale : -__builtin_huge_val();
+        for (int j = 0; j < KPG; ++j) {
+            s[j] = k0 + KPG * g + j < Nk ? s[j] * p.scale : -__builtin_huge_val();
             mx = dmax(mx, s[j]);
         }
-        red[g * kQB64 + qi] = mx;
+        red[g * QB + qi] = mx;
         __syncthreads();
         // online update (src/dense.jl:78-91): every thread of query qi holds the same m, l
-        const double tmax = dmax(dmax(red[qi], red[kQB64 + qi]), dmax(red[2 * kQB64 + qi], red[3 * kQB64 + qi]));
+        double tmax = red[qi];
+#pragma unroll
+        for (int gg = 1; gg < NG; ++gg) tmax = dmax(tmax, red[gg * QB + qi]);
         const double m_new = dmax(m_run, tmax);
         const double alpha = exp(m_run - m_new);
         double ps = 0.0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < KPG; ++j) {
             const double pj = exp(s[j] - m_new);
             ps += pj;
-            if (!STATS) sP[qi * (kKB64 + 1) + 8 * g + j] = pj;
+            if (!STATS) sP[qi * (kKB64 + 1) + KPG * g + j] = pj;
         }
-        red[4 * kQB64 + g * kQB64 + qi] = ps;
+        red[kTh64 + g * QB + qi] = ps;
         __syncthreads();
-        l_run = l_run * alpha + ((red[4 * kQB64 + qi] + red[5 * kQB64 + qi]) +
-                                 (red[6 * kQB64 + qi] + red[7 * kQB64 + qi]));
+        double lt = 0.0;
+#pragma unroll
+        for (int gg = 0; gg < NG; ++gg) lt += red[kTh64 + gg * QB + qi];
+        l_run = l_run * alpha + lt;
         m_run = m_new;
         if (!STATS) {
             double pr[kKB64];
 #pragma unroll
             for (int k = 0; k < kKB64; ++k) pr[k] = sP[qi * (kKB64 + 1) + k];
 #pragma unroll
-            for (int i = 0; i < kOPer64; ++i) {
-                const int c = g + 4 * i;
+            for (int i = 0; i < OPER; ++i) {
+                const int c = g + NG * i;
                 if (c < dv) {
                     const double* vr = sV + c * kKB64;
                     double acc = o[i] * alpha;
@@ -147,8 +156,8 @@ __global__ __launch_bounds__(kTh64) void dense_fwd_f64(F64Params p) {
     const double inv = 1.0 / l_run;
     double* Ob = p.O + (int64_t)b * N * dv;
 #pragma unroll
-    for (int i = 0; i < kOPer64; ++i) {
-        const int c = g + 4 * i;
+    for (int i = 0; i < OPER; ++i) {
+        const int c = g + NG * i;
         if (c < dv) Ob[(int64_t)c * N + n] = o[i] * inv;
     }
     if (g == 0) {
@@ -182,12 +191,21 @@ static bool f64_fits(int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch
     return true;
 }
 
+template <bool STATS, int QB>
+static hipError_t launch_f64_qb(F64Params p, int64_t batch, hipStream_t s) {
+    p.nqb = (p.N + QB - 1) / QB;
+    const size_t lds = f64_lds_bytes(p.d, p.dv, STATS, QB);
+    (void)hipFuncSetAttribute((const void*)dense_fwd_f64<STATS, QB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL((dense_fwd_f64<STATS, QB>), dim3((unsigned)(p.nqb * batch)), dim3(kTh64), lds, s, p);
+    return hipGetLastError();
+}
+// 64 queries per workgroup when that fills the chip, else 16 (4x the workgroups:
+// the reference's own Float64 cases are single slabs of 256-16384 tokens)
 template <bool STATS>
 static hipError_t launch_f64_kernel(const F64Params& p, int64_t batch, hipStream_t s) {
-    const size_t lds = f64_lds_bytes(p.d, p.dv, STATS);
-    (void)hipFuncSetAttribute((const void*)dense_fwd_f64<STATS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(dense_fwd_f64<STATS>, dim3((unsigned)(p.nqb * batch)), dim3(kTh64), lds, s, p);
-    return hipGetLastError();
+    if ((int64_t)((p.N + kQB64 - 1) / kQB64) * batch >= 256) return launch_f64_qb<STATS, kQB64>(p, batch, s);
+    return launch_f64_qb<STATS, 16>(p, batch, s);
 }
 
 int launch_dense_fwd_f64(const DenseArgs& a, hipStream_t s, const char** why) {
