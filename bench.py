@@ -22,20 +22,39 @@ Timing protocol:
   3. the GPU clock and board power are sampled (amdsmi via torch.cuda) during
      the timed region and reported ("clock").
 
-Secondary blocks on the same JSON line (never the headline `value`):
-  * "cfg5": BASELINE configs[4] = (64,16,16384,128) bf16 forward, STRONG
-    scaling: its 1024 (B·H) slabs are split over the N ranks
-    (fa_hip.shard.shard_range), each rank times its share; total TFLOP/s =
-    all ranks' FLOPs / the slowest rank's time.
+Secondary blocks on the same JSON line (never the headline `value`), keyed by
+the BASELINE.json configs index they measure:
+  * "cfg2": configs[2] = windowed_fa 2-D bf16, 128x128 image, ws 7, d 64:
+    forward and backward at B = 1 (as written) and B = 32, GB/s against the
+    8 TB/s HBM roofline (HIP-graph replay: launch-bound at B = 1);
+  * "cfg3": configs[3] = (4,16,8192,128) bf16 forward, backward and
+    forward+backward TFLOP/s, each with its own MFMA roofline (2.5x / 3.5x the
+    forward FLOPs), and whether the single-pass backward's dQ
+    hand-off fell back (fa_dense_bwd_handoff_status);
+  * "cfg4": configs[4] = (64,16,16384,128) bf16 forward, STRONG scaling: its
+    1024 (B·H) slabs are split over the N ranks (fa_hip.shard.shard_range),
+    each rank times its share; total TFLOP/s = all ranks' FLOPs / the slowest
+    rank's time.
   * "cpu_baseline" (rank 0, N = 1): the reference's CPU algorithm
     (oracle/fa_cpu.c BLAS port of dense_fa!) on configs[0] at 1 thread and at
     the process's cores (median of 50 after 5 warm-ups), the reference's own
     published Float64 case (512, 64, 1) likewise, and the whole configs[1]
     workload (fp32).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-cfg5] [--extra]
-Multi-GPU: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
-           --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-cfg4] [--no-cfg23] [--extra]
+Multi-GPU: `python bench.py --gpus N` (N > 1, WORLD_SIZE unset) starts N ranks
+           itself as a child `python -m torch.distributed.run --nnodes=1
+           --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...`
+           (before any GPU call; the parent only waits and exits with the
+           child's code, rank 0 prints the JSON line).  Launched by
+           torch.distributed.run directly, --gpus must equal WORLD_SIZE
+           (exit 2 otherwise).
+
+Test hook (CPU only, never on a GPU run): FA_BENCH_CPU_STEP=1 replaces every
+device step by a CPU stand-in (rank r sleeps (r + 1) * 5 ms per step) so that
+tests/test_bench_dist.py can run the literal `python bench.py --gpus 2` with
+FA_BENCH_BACKEND=gloo and check the launch, world, slab split and MAX
+reduction; the JSON then says "cpu_step_hook": true.
 """
 from __future__ import annotations
 
@@ -60,7 +79,7 @@ PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12   # 2516.6: 256 CU x 2.4 GHz x 4096
 PEAK_HBM_GBS = 8000.0
 B_, H_, N_, D_ = 4, 16, 4096, 64
 # BASELINE configs[4]: (B,H,N,d) = (64,16,16384,128), sharded over (B·H)
-CFG5_SLABS, CFG5_N, CFG5_D = 64 * 16, 16384, 128
+CFG4_SLABS, CFG4_N, CFG4_D = 64 * 16, 16384, 128
 
 
 # ----------------------------------------------------------------------------
@@ -229,23 +248,110 @@ def _randn_jl(fa, shape, dtype, gen):
     return t
 
 
-def cfg5_block(fa, world, rank, dist, steps, warmup):
+def cfg4_block(fa, world, rank, dist, steps, warmup, cpu_hook=False):
     """BASELINE configs[4]: dense_fa bf16 forward (N, d) = (16384, 128) over
     1024 (B·H) slabs, split over the ranks (strong scaling)."""
-    gen = torch.Generator(device="cuda").manual_seed(4242 + rank)
-    N, d = CFG5_N, CFG5_D
+    N, d = CFG4_N, CFG4_D
+    if cpu_hook:
+        make_step = lambda n: _cpu_hook_step(rank)
+        r = sharded_strong(make_step, CFG4_SLABS, world, rank, dist, steps, warmup, 4.0 * N * N * d,
+                           sync=lambda: None, events=False)
+    else:
+        gen = torch.Generator(device="cuda").manual_seed(4242 + rank)
 
-    def make_step(n):
-        Q, K, V = (_randn_jl(fa, (N, d, n), torch.bfloat16, gen) for _ in range(3))
-        O = fa.jl_empty((N, d, n), torch.bfloat16)
-        l = fa.jl_empty((N, 1, n))
-        m = fa.jl_empty((N, 1, n))
-        return lambda: fa.dense_fa_(O, l, m, Q, K, V)
+        def make_step(n):
+            Q, K, V = (_randn_jl(fa, (N, d, n), torch.bfloat16, gen) for _ in range(3))
+            O = fa.jl_empty((N, d, n), torch.bfloat16)
+            l = fa.jl_empty((N, 1, n))
+            m = fa.jl_empty((N, 1, n))
+            return lambda: fa.dense_fa_(O, l, m, Q, K, V)
 
-    r = sharded_strong(make_step, CFG5_SLABS, world, rank, dist, steps, warmup, 4.0 * N * N * d)
+        r = sharded_strong(make_step, CFG4_SLABS, world, rank, dist, steps, warmup, 4.0 * N * N * d)
+        torch.cuda.empty_cache()
     r["workload"] = "configs[4]: dense_fa bf16 forward, (B,H,N,d)=(64,16,16384,128), 1024 slabs split over ranks"
-    torch.cuda.empty_cache()
+    r["kernel"] = "fa::dense_fwd_w8b64_wide<bf16,128,128>"
     return r
+
+
+def _mfma_roofline(flops, seconds, kernel, note=None):
+    ach = flops / seconds / 1e12
+    r = {"bound": "mfma", "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+         "frac": ach / PEAK_BF16_TFLOPS, "kernel": kernel, "flops_per_launch": flops,
+         "avg_launch_ms": seconds * 1e3}
+    if note:
+        r["note"] = note
+    return r
+
+
+def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
+    """BASELINE configs[3]: dense_fa bf16 (B,H,N,d) = (4,16,8192,128) forward,
+    backward (reference src/dense.jl:104-167, executable spec
+    src_cpp/FlashAttention.cpp:194-252) and forward+backward.  FLOPs: forward
+    4·BH·N²·d, backward 2.5x, fwd+bwd 3.5x.  Device time by
+    HIP events on the launch stream; ~60 ms of GPU time."""
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    N, d, BH = 8192, 128, 64
+    Q, K, V, dO = (_randn_jl(fa, (N, d, BH), torch.bfloat16, gen) for _ in range(4))
+    O = fa.jl_empty((N, d, BH), torch.bfloat16)
+    l = fa.jl_empty((N, 1, BH))
+    m = fa.jl_empty((N, 1, BH))
+    f = 4.0 * BH * N * N * d
+    _, e_f = time_region(lambda: fa.dense_fa_(O, l, m, Q, K, V), steps_fwd, 2, dist)
+    t_f = e_f / steps_fwd
+    _, e_b = time_region(lambda: fa.dense_fa_backward(Q, K, V, O, dO, l, m), steps_bwd, 1, dist)
+    t_b = e_b / steps_bwd
+    hs = fa.backward_handoff_status(Q.device)
+    res = {
+        "workload": "configs[3]: dense_fa bf16 forward + backward, (B,H,N,d)=(4,16,8192,128)",
+        "fwd_tflops": f / t_f / 1e12, "bwd_tflops": 2.5 * f / t_b / 1e12,
+        "fwd_bwd_tflops": 3.5 * f / (t_f + t_b) / 1e12,
+        "fwd_ms": t_f * 1e3, "bwd_ms": t_b * 1e3, "steps_fwd": steps_fwd, "steps_bwd": steps_bwd,
+        "roofline_fwd": _mfma_roofline(f, t_f, "fa::dense_fwd_w8b64_wide<bf16,128,128>"),
+        "roofline_bwd": _mfma_roofline(
+            2.5 * f, t_b, "fa::bwd_fused<bf16,128,128>",
+            "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + bwd_fused + the guarded dQ pass), "
+            "FLOPs = 2.5x forward (the 5 GEMMs bwd_fused executes)"),
+        "roofline_fwd_bwd": _mfma_roofline(3.5 * f, t_f + t_b, "forward + backward calls"),
+        "bwd_handoff": {-1: "two-pass plan (no hand-off)", 0: "single pass, hand-off completed",
+                        1: "single pass, hand-off TIMED OUT: dQ recomputed by the guarded pass"}.get(hs, hs),
+    }
+    del Q, K, V, dO, O, l, m
+    torch.cuda.empty_cache()
+    return res
+
+
+def cfg2_block(fa, dist, steps=20):
+    """BASELINE configs[2]: windowed_fa 2-D bf16, 128x128 image, ws 7 (stride 7,
+    pad 3: 19x19 windows of 49 tokens), d 64 (reference src/windowed.jl:3-23,
+    src/utils.jl:36-54); forward and backward at B = 1 (as written) and
+    B = 32.  HBM-bound (26 FLOP/B): algorithmic bytes = q, k, v read + y
+    written (+ l, m) for the forward; q, k, v, y, dy read + dq, dk, dv written
+    (+ l, m) for the backward; GB/s against 8 TB/s."""
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    T, L, S, dd = 49, 19 * 19, 128 * 128, 64
+    res = {"workload": "configs[2]: windowed_fa 2-D bf16, 128x128 image, ws=7, d=64, stride 7, pad 3",
+           "timing": "HIP-graph replay of back-to-back calls (device time per call)"}
+    for Bimg in (1, 32):
+        q, k, v, dy = (_randn_jl(fa, (128, 128, dd, Bimg), torch.bfloat16, gen) for _ in range(4))
+        t = time_graph(lambda: fa.windowed_fa(q, k, v, 7), steps, dist)
+        by = Bimg * (4 * S * dd * 2 + 2 * T * L * 4)
+        y, lw, mw = fa.windowed_fa(q, k, v, 7)
+        tb = time_graph(lambda: fa.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), max(5, steps // 2), dist)
+        bb = Bimg * (8 * S * dd * 2 + 2 * T * L * 4)
+        res[f"B{Bimg}"] = {
+            "fwd_us": t * 1e6, "fwd_GBs": by / t / 1e9, "fwd_frac_hbm": by / t / 1e9 / PEAK_HBM_GBS,
+            "fwd_bytes": by, "fwd_kernel": "fa::win_rows1s<bf16,64,64,2>",
+            "bwd_us": tb * 1e6, "bwd_GBs": bb / tb / 1e9, "bwd_frac_hbm": bb / tb / 1e9 / PEAK_HBM_GBS,
+            "bwd_bytes": bb, "bwd_kernel": "fa::win_bwd_rows<bf16,64,64>"}
+        del q, k, v, dy, y, lw, mw
+    torch.cuda.empty_cache()
+    return res
+
+
+def _cpu_hook_step(rank):
+    """FA_BENCH_CPU_STEP=1 stand-in for a device step (tests only): rank r
+    sleeps (r + 1) * 5 ms, so the MAX over ranks is the last rank's time."""
+    return lambda: time.sleep(0.005 * (rank + 1))
 
 
 def _cpu_model():
@@ -261,29 +367,38 @@ def _cpu_model():
 def _cpu_threads():
     """Cores this process may use: its affinity set, capped by the box's
     OMP_NUM_THREADS share when set (the GPU box exports 16 per GPU)."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n = _node_cpus()
     env = os.environ.get("OMP_NUM_THREADS")
     if env and env.isdigit() and int(env) > 0:
         n = min(n, int(env))
     return max(1, n)
 
 
+def _node_cpus():
+    """Every host CPU this process may run on (sched_getaffinity): the node's
+    cores as north_star's CPU baseline asks for."""
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
 def cpu_baseline():
     """The reference's CPU algorithm, dense_fa! (src/dense.jl:21-102), as the
     BLAS-backed C/OpenMP port oracle/fa_cpu.c (same Br/Bc tiles, one gemm per
-    tile product, (slab x row-block) tasks), fp32:
-      * configs[0] (N,d,B·H) = (512,64,4): 1 thread and all usable cores,
-        median of 50 after 5 warm-ups (BASELINE.md 'CPU baseline plan');
-      * configs[1] (4096,64,64): the whole workload at all usable cores, median
-        of 3 after 1 warm-up -> `value` (same unit as the headline)."""
+    tile product, (slab x row-block) tasks), fp32, at two thread counts:
+      * "node": every CPU of the process's affinity set (the node's host cores,
+        north_star) -> `value` / `cores`;
+      * "share": the box's per-GPU OMP_NUM_THREADS share (16 on the GPU box).
+    Each leg times configs[0] (N,d,B·H) = (512,64,4) (median of 50 after 5
+    warm-ups; also at 1 thread), the reference's own published Float64 case
+    (512,64,1) (logs/compare1.txt:4), and the whole configs[1] workload
+    (4096,64,64) (median of 3 after 1 warm-up)."""
     import numpy as np
     from oracle import cpu_port
     cpu_port.blas_info()
-    threads = _cpu_threads()
+    node, share = _node_cpus(), _cpu_threads()
     rng = np.random.default_rng(0)
 
-    def arrs(N, d, n):
-        return [np.asfortranarray(rng.standard_normal((N, d, n)).astype(np.float32)) for _ in range(3)]
+    def arrs(N, d, n, dt=np.float32):
+        return [np.asfortranarray(rng.standard_normal((N, d, n)).astype(dt)) for _ in range(3)]
 
     def med_time(fn, reps, warm):
         for _ in range(warm):
@@ -296,30 +411,31 @@ def cpu_baseline():
         return statistics.median(ts)
 
     q0, k0, v0 = arrs(512, 64, 4)
-    f0 = 4.0 * 4 * 512 * 512 * 64
-    c0 = {}
-    for th in sorted({1, threads}):
-        t = med_time(lambda: cpu_port.dense_fa_blas(q0, k0, v0, th), 50, 5)
-        c0[f"threads_{th}"] = {"ms": t * 1e3, "gflops": f0 / t / 1e9}
-    # the reference's own published case, as it ran it: Float64, (N, d, bs) = (512, 64, 1)
-    # (logs/compare1.txt:4: 2.392 ms), 1 thread and all usable cores
-    qr, kr, vr = (np.asfortranarray(rng.standard_normal((512, 64, 1))) for _ in range(3))
-    fr = 4.0 * 512 * 512 * 64
-    cr = {}
-    for th in sorted({1, threads}):
-        t = med_time(lambda: cpu_port.dense_fa_blas(qr, kr, vr, th), 50, 5)
-        cr[f"threads_{th}"] = {"ms": t * 1e3, "gflops": fr / t / 1e9}
+    qr, kr, vr = arrs(512, 64, 1, np.float64)
     q1, k1, v1 = arrs(N_, D_, B_ * H_)
-    t1 = med_time(lambda: cpu_port.dense_fa_blas(q1, k1, v1, threads), 3, 1)
-    f1 = 4.0 * B_ * H_ * N_ * N_ * D_
-    return {"value": f1 / t1 / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
-            "cpu_model": _cpu_model(),
-            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+    f0, fr, f1 = 4.0 * 4 * 512 * 512 * 64, 4.0 * 512 * 512 * 64, 4.0 * B_ * H_ * N_ * N_ * D_
+    legs = {}
+    for tag, th in (("node", node), ("share", share)):
+        if tag == "share" and share == node:
+            legs[tag] = "same thread count as the node leg"
+            continue
+        c0 = {}
+        for t_ in sorted({1, th}):
+            t = med_time(lambda: cpu_port.dense_fa_blas(q0, k0, v0, t_), 50, 5)
+            c0[f"threads_{t_}"] = {"ms": t * 1e3, "gflops": f0 / t / 1e9}
+        tr = med_time(lambda: cpu_port.dense_fa_blas(qr, kr, vr, th), 50, 5)
+        t1 = med_time(lambda: cpu_port.dense_fa_blas(q1, k1, v1, th), 3, 1)
+        legs[tag] = {"threads": th, "configs1_fp32_tflops": f1 / t1 / 1e12, "configs1_s": t1,
+                     "configs0_fp32_512x64x4": c0,
+                     "reference_case_f64_512x64x1": {"ms": tr * 1e3, "gflops": fr / tr / 1e9}}
+    nl = legs["node"]
+    return {"value": nl["configs1_fp32_tflops"], "unit": "TFLOP/s", "cores": node, "kind": "port",
+            "cpu_model": _cpu_model(), "affinity_cpus": node, "omp_share": share,
             "sample": f"the whole configs[1] workload (4096,64,64) fp32, BLAS-backed C/OpenMP port of dense_fa! "
-                      f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles, OpenBLAS sgemm per tile product, {threads} threads), "
-                      f"median of 3: {t1:.2f} s",
-            "configs0_fp32_512x64x4": c0,
-            "reference_case_f64_512x64x1": cr,
+                      f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles, OpenBLAS sgemm per tile product) on all {node} "
+                      f"affinity CPUs, median of 3: {nl['configs1_s']:.3f} s; 'legs' adds the per-GPU "
+                      f"{share}-thread share, configs[0] and the reference's Float64 case",
+            "legs": legs,
             "reference_published": "dense_fa Julia N=512 d=64 bs=1 Float64: 2.392 ms, unstated CPU "
                                    "(/root/reference/logs/compare1.txt:4)"}
 
@@ -341,6 +457,30 @@ def _traffic_from_profiles():
     return best
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a torch.distributed.run environment: start
+    the N ranks as ONE child process tree (python -m torch.distributed.run,
+    rendezvous on 127.0.0.1) and return its exit code.  Called before anything
+    touches the GPU; the parent never re-execs itself, it only waits (rank 0's
+    JSON line reaches stdout directly)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -348,33 +488,56 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--settle-ms", type=float, default=250.0,
                     help="untimed back-to-back launches before timing (disclosed in the JSON)")
-    ap.add_argument("--cfg5-steps", type=int, default=3)
+    ap.add_argument("--cfg4-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--no-cfg5", action="store_true", help="skip the configs[4] strong-scaling block")
-    ap.add_argument("--extra", action="store_true", help="also time configs[2..3] (reported under 'extra')")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the configs[4] strong-scaling block")
+    ap.add_argument("--no-cfg23", action="store_true", help="skip the configs[2] / configs[3] blocks")
+    ap.add_argument("--extra", action="store_true", help="also time the secondary paths (reported under 'extra')")
     args = ap.parse_args()
+    if args.gpus < 1:
+        print(f"bench.py: --gpus must be >= 1 (got {args.gpus})", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU "
+              f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop --gpus", file=sys.stderr)
+        return 2
 
-    dist, rank, world, local = dist_init()
-    import fa_hip
-    fa_hip.lib()
+    cpu_hook = os.environ.get("FA_BENCH_CPU_STEP") == "1"
+    if cpu_hook and torch.cuda.is_available():
+        print("bench.py: FA_BENCH_CPU_STEP is a CPU test hook; refusing it on a GPU box", file=sys.stderr)
+        return 2
+    dist, rank, world, local = dist_init("gloo" if cpu_hook else None)
 
+    if cpu_hook:
+        fa_hip = None
+        step = _cpu_hook_step(rank)
+        sync, events = (lambda: None), False
+    else:
+        import fa_hip
+        fa_hip.lib()
+        BH = B_ * H_
+        gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+        Q = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
+        K = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
+        V = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
+        O = fa_hip.jl_empty((N_, D_, BH), torch.bfloat16)
+        l = fa_hip.jl_empty((N_, 1, BH), torch.float32)
+        m = fa_hip.jl_empty((N_, 1, BH), torch.float32)
+        step = lambda: fa_hip.dense_fa_(O, l, m, Q, K, V)
+        sync, events = _cuda_sync, True
     BH = B_ * H_
-    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
-    Q = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
-    K = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
-    V = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
-    O = fa_hip.jl_empty((N_, D_, BH), torch.bfloat16)
-    l = fa_hip.jl_empty((N_, 1, BH), torch.float32)
-    m = fa_hip.jl_empty((N_, 1, BH), torch.float32)
-    step = lambda: fa_hip.dense_fa_(O, l, m, Q, K, V)
     flops_rank = 4.0 * BH * N_ * N_ * D_
+    sampler = (lambda: _NullSampler()) if cpu_hook else (lambda: ClockSampler(torch.cuda.current_device()))
 
     # cold: exactly W warm-up steps from idle, then the K timed steps
-    wall_c, ev_c = time_region(step, args.steps, args.warmup, dist)
-    with ClockSampler(torch.cuda.current_device()) as clk_settle:   # sustained load: many samples
-        settle_n, settle_s = settle(step, args.settle_ms / 1e3)
-    with ClockSampler(torch.cuda.current_device()) as clk:
-        wall, ev_s = time_region(step, args.steps, args.warmup, dist)
+    wall_c, ev_c = time_region(step, args.steps, args.warmup, dist, sync, events)
+    with sampler() as clk_settle:   # sustained load: many samples
+        settle_n, settle_s = settle(step, (0.0 if cpu_hook else args.settle_ms) / 1e3, sync)
+    with sampler() as clk:
+        wall, ev_s = time_region(step, args.steps, args.warmup, dist, sync, events)
     value = flops_rank * world * args.steps / wall / 1e12
     kern_s = ev_s / args.steps
     achieved = flops_rank / kern_s / 1e12
@@ -402,14 +565,19 @@ def main():
         # runs the same launches back to back for --settle-ms and is sampled throughout
         "clock_settle": clk_settle.summary(),
     }
+    if cpu_hook:
+        out["cpu_step_hook"] = True
 
-    if not args.no_cfg5:
-        out["cfg5"] = cfg5_block(fa_hip, world, rank, dist, args.cfg5_steps, 1)
+    if not args.no_cfg23 and not cpu_hook:
+        out["cfg3"] = cfg3_block(fa_hip, dist)
+        out["cfg2"] = cfg2_block(fa_hip, dist)
+    if not args.no_cfg4:
+        out["cfg4"] = cfg4_block(fa_hip, world, rank, dist, args.cfg4_steps, 1, cpu_hook)
 
-    if args.extra:
+    if args.extra and not cpu_hook:
         out["extra"] = extra_benches(fa_hip, args, dist)
 
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not cpu_hook:
         out["cpu_baseline"] = cpu_baseline()
     elif rank == 0:
         out["cpu_baseline"] = None
@@ -418,6 +586,18 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
+
+
+class _NullSampler:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+    def summary(self):
+        return None
 
 
 def time_graph(fn, steps, dist=None):
@@ -520,4 +700,4 @@ def extra_benches(fa_hip, args, dist):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -128,13 +128,20 @@ int fa_debug_set_bwd_generic(int v) {
 
 // Not part of the public header: backward MFMA path (0 auto, 1 the dK/dV + dQ
 // passes, 2 the single pass wherever its shape conditions hold, 3 as 2 with the
-// hand-off's timeout word preset, which exercises the dQ fallback pass; 4, 5, 6:
-// timing-only ablations of the single pass with WRONG dQ: no waits, no running-sum
-// traffic, neither; 7, 8: no running-sum loads / no running-sum stores; 9: no dS
-// image writes).
+// hand-off's timeout word preset, which exercises the dQ fallback pass).  Builds with
+// -DFA_BWD_ABL also accept the timing-only ablations of the single pass, which compute
+// a WRONG dQ: 4, 5, 6 no waits, no running-sum traffic, neither; 7, 8 no running-sum
+// loads / stores; 9 no dS image writes.  Any other value is rejected (returns -1, the
+// mode is unchanged).
 int fa_debug_set_bwd_mode(int v) {
     const int old = fa::g_bwd_mode;
-    fa::g_bwd_mode = (v >= 1 && v <= 9) ? v : 0;
+#ifdef FA_BWD_ABL
+    constexpr int kMaxMode = 9;
+#else
+    constexpr int kMaxMode = 3;
+#endif
+    if (v < 0 || v > kMaxMode) return -1;
+    fa::g_bwd_mode = v;
     return old;
 }
 
@@ -237,6 +244,14 @@ int fa_dense_bwd(int dtype, const void* Q, const void* K, const void* V, const v
     a.scale64 = resolve_scale64(scale, d);
     const char* why = "";
     const int rc = fa::launch_dense_bwd(a, (hipStream_t)hip_stream, &why);
+    return rc == FA_OK ? ok() : fail(rc, fn, why);
+}
+
+int fa_dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes, void* hip_stream, int* status) {
+    static const char* fn = "fa_dense_bwd_handoff_status";
+    if (!status) return fail(FA_ERR_INVALID_ARG, fn, "null status pointer");
+    const char* why = "";
+    const int rc = fa::dense_bwd_handoff_status(workspace, workspace_bytes, (hipStream_t)hip_stream, status, &why);
     return rc == FA_OK ? ok() : fail(rc, fn, why);
 }
 

@@ -38,7 +38,11 @@ struct BwdParams {
     double scale64 = 0.0;        // Float64 generic path: τ in double
     // single-pass kernel (bwd_fused): dQ hand-off state, all in the caller's workspace
     unsigned* flags = nullptr;   // [batch][nqt] members that have published slice t (zeroed per call)
-    unsigned* err = nullptr;     // hand-off timeout flag (zeroed per call)
+    unsigned* err = nullptr;     // hand-off timeout word = hdr[1] (set per call by the pre-pass)
+    // workspace header (first 256 B of the aligned workspace; fa_dense_bwd_handoff_status):
+    // hdr[0] = kBwdHdrMagic | plan (1 = single pass), hdr[1] = the timeout word
+    unsigned* hdr = nullptr;
+    unsigned hdr_plan = 0, hdr_err = 0;
     float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
     int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
@@ -46,6 +50,18 @@ struct BwdParams {
 };
 
 template <class T> __device__ __forceinline__ float to_f(T x) { return (float)x; }
+
+constexpr unsigned kBwdHdrMagic = 0x46414200u;   // "FAB\0"
+constexpr size_t kBwdHdrBytes = 256;
+
+// The pre-pass runs first on the stream in every 16/32-bit backward: its thread 0
+// (re)writes the workspace header, so the timeout word starts each call at hdr_err.
+__device__ __forceinline__ void write_bwd_header(const BwdParams& p) {
+    if (p.hdr) {
+        p.hdr[0] = kBwdHdrMagic | p.hdr_plan;
+        p.hdr[1] = p.hdr_err;
+    }
+}
 
 // --------------------------------------------------------------------------
 // 1. pre-pass (HBM-bound): one thread per (b, n), coalesced along n.
@@ -55,6 +71,7 @@ __global__ __launch_bounds__(256) void bwd_prepass(BwdParams p) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t total = (int64_t)p.N * p.batch;
     if (idx >= total) return;
+    if (idx == 0) write_bwd_header(p);
     const int64_t b = idx / p.N, n = idx - b * p.N;
     const T* O = (const T*)p.O + b * (int64_t)p.N * p.dv + n;
     const T* dO = (const T*)p.dO + b * (int64_t)p.N * p.dv + n;
@@ -73,6 +90,7 @@ __global__ __launch_bounds__(256) void bwd_prepass_v(BwdParams p) {
     constexpr int U = 8;
     const int64_t g8 = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g8 >= (int64_t)p.N * p.batch / 8) return;
+    if (g8 == 0) write_bwd_header(p);
     const int64_t idx = g8 * 8, b = idx / p.N, n = idx - b * p.N;
     const T* O = (const T*)p.O + b * (int64_t)p.N * p.dv + n;
     const T* dO = (const T*)p.dO + b * (int64_t)p.N * p.dv + n;
@@ -1214,35 +1232,47 @@ struct FusedPlan {
     int nkb = 0, nqt = 0, xcd = 0;
     size_t flag_bytes = 0, bytes = 0;
 };
-static int device_cus() {
+// CUs of the device the work runs on: the stream's device (the current device for
+// the NULL stream, and for fa_dense_bwd_workspace, which takes no stream).
+static int device_cus(hipStream_t s) {
     int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    if (s != nullptr) {
+        if (hipStreamGetDevice(s, &dev) != hipSuccess) return 0;
+    } else if (hipGetDevice(&dev) != hipSuccess) {
         return 0;
+    }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     return cus;
 }
-static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
+static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
+                            hipStream_t s = nullptr) {
     FusedPlan f;
     if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
-    const int cus = device_cus();
+    const int cus = device_cus(s);
     if (cus < 8 || 3 * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
-    if ((g_bwd_mode == 0 || g_bwd_mode == 1) && batch * K < cus) return f;
+    const int xcd = (K <= cus / 8 && batch % 8 == 0) ? 1 : 0;
+    if (g_bwd_mode == 0) {
+        // auto: the grid fills the chip, and K divides the CUs a slab's members are dealt
+        // over (one XCD's, or the chip's), so no slab waits part-resident behind another
+        if (batch * K < cus || (xcd ? cus / 8 : cus) % K != 0) return f;
+    }
     f.on = true;
     f.nkb = (int)K;
     f.nqt = (int)T;
-    f.xcd = (K <= cus / 8 && batch % 8 == 0) ? 1 : 0;
-    f.flag_bytes = al256((size_t)(batch * T) * 4) + 256;
+    f.xcd = xcd;
+    f.flag_bytes = al256((size_t)(batch * T) * 4);
     f.bytes = f.flag_bytes + al256((size_t)(batch * T * (d / 16)) * 4096) + 256;
     return f;
 }
 
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
-    if (dtype == FA_DTYPE_F64) return (size_t)(2 * N * batch * sizeof(double) + 256);   // nD, nlse in double
+    if (dtype == FA_DTYPE_F64) return kBwdHdrBytes + (size_t)(2 * N * batch * sizeof(double) + 256);   // nD, nlse in double
     const BwdPad pl = pad_plan(dtype, N, Nk, d, dv, batch);
     const int64_t rows = pl.on ? pl.Np : N;
     const FusedPlan fz = pl.on ? fused_plan(dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp, batch)
                                : fused_plan(dtype, N, Nk, d, dv, batch);
-    return (size_t)(2 * rows * batch * sizeof(float) + 256) + (pl.on ? pl.bytes + 256 : 0) + fz.bytes;
+    return kBwdHdrBytes + (size_t)(2 * rows * batch * sizeof(float) + 256) + (pl.on ? pl.bytes + 256 : 0) + fz.bytes;
 }
 
 // dst (Np, Cp, B) <- src (N, C, B), zero-filled
@@ -1333,6 +1363,44 @@ static hipError_t launch_typed(const BwdParams& p, hipStream_t s, bool fast) {
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
+// Single-pass state in the workspace at w: per-slice counters (zeroed here), then the
+// running dQ sums.  The timeout word is hdr[1], which the pre-pass sets to hdr_err.
+static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStream_t s) {
+    p.flags = (unsigned*)w;
+    p.part = (float*)(w + fz.flag_bytes);
+    p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
+    p.hdr_plan = 1;
+    // mode 3 (tests): the timeout word starts set, so every poll gives up and the
+    // guarded dQ pass must recompute dQ
+    p.hdr_err = g_bwd_mode == 3 ? 1u : 0u;
+#ifdef FA_BWD_ABL
+    p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
+#endif
+    return hipMemsetAsync(w, 0, fz.flag_bytes, s);
+}
+
+int dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes, hipStream_t s, int* status,
+                             const char** why) {
+    const uintptr_t ws0 = ((uintptr_t)workspace + 255) & ~(uintptr_t)255;
+    if (!workspace || ws0 + 8 > (uintptr_t)workspace + workspace_bytes) {
+        *why = "workspace missing or smaller than its header";
+        return FA_ERR_INVALID_ARG;
+    }
+    unsigned h[2] = {0u, 0u};
+    hipError_t e = hipMemcpyAsync(h, (const void*)ws0, sizeof(h), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return FA_ERR_HIP;
+    }
+    if ((h[0] & 0xFFFFFF00u) != kBwdHdrMagic) {
+        *why = "workspace holds no fa_dense_bwd header (not the workspace of an fa_dense_bwd call)";
+        return FA_ERR_INVALID_ARG;
+    }
+    *status = (h[0] & 0xFFu) == 1u ? (h[1] != 0u ? 1 : 0) : -1;
+    return FA_OK;
+}
+
 int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
         *why = "head dimension exceeds the compiled maximum (128)";
@@ -1346,7 +1414,10 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
     BwdParams p;
     p.Q = a.Q; p.K = a.K; p.V = a.V; p.O = a.O; p.dO = a.dO; p.l = a.l; p.m = a.m;
     p.dQ = a.dQ; p.dK = a.dK; p.dV = a.dV;
-    const uintptr_t ws = ((uintptr_t)a.workspace + 255) & ~(uintptr_t)255;
+    const uintptr_t ws0 = ((uintptr_t)a.workspace + 255) & ~(uintptr_t)255;
+    p.hdr = (unsigned*)ws0;
+    p.err = p.hdr + 1;
+    const uintptr_t ws = ws0 + kBwdHdrBytes;
     p.nD = (float*)ws;
     p.nlse = p.nD + a.N * a.batch;
     p.N = (int)a.N; p.Nk = (int)a.Nk; p.d = (int)a.d; p.dv = (int)a.dv; p.batch = (int)a.batch;
@@ -1362,6 +1433,10 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
         }
         double* nD = (double*)ws;
         double* nlse = nD + a.N * a.batch;
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)p.hdr, kBwdHdrMagic, 1, s)) != hipSuccess) {   // plan 0
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
         p.nD = (float*)nD;
         p.nlse = (float*)nlse;
         p.scale64 = a.scale64 > 0.0 ? a.scale64 : (double)a.scale;
@@ -1395,20 +1470,11 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
             *why = "workspace smaller than fa_dense_bwd_workspace()";
             return FA_ERR_WORKSPACE;
         }
-        const FusedPlan fz = fused_plan(a.dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp, B);
-        if (fz.on && (size_t)(w - (char*)a.workspace) + fz.bytes <= a.workspace_bytes) {
-            p.flags = (unsigned*)w;
-            p.err = (unsigned*)(w + fz.flag_bytes - 256);
-            p.part = (float*)(w + fz.flag_bytes);
-            p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
-            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
-            // mode 3 (tests): the timeout word starts set, so every poll gives up
-            // and the guarded dQ pass must recompute dQ
-            if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
-                (g_bwd_mode == 3 && (e = hipMemsetAsync(p.err, 1, 4, s)) != hipSuccess)) {
-                *why = hipGetErrorString(e);
-                return FA_ERR_HIP;
-            }
+        const FusedPlan fz = fused_plan(a.dtype, pl.Np, pl.Nkp, pl.Dp, pl.DVp, B, s);
+        if (fz.on && (size_t)(w - (char*)a.workspace) + fz.bytes <= a.workspace_bytes &&
+            (e = fused_setup(p, fz, w, s)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
         }
         const bool half = a.dtype == FA_DTYPE_F16;
         auto pad = [&](const void* src, void* dst, int64_t N, int64_t C, int64_t Np, int64_t Cp) {
@@ -1444,21 +1510,12 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
         return FA_OK;
     }
     if (fast) {
-        const FusedPlan fz = fused_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
+        const FusedPlan fz = fused_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch, s);
         char* w = (char*)ws + al256((size_t)(2 * a.N * a.batch) * sizeof(float));
-        if (fz.on && (size_t)(w - (char*)a.workspace) + fz.bytes <= a.workspace_bytes) {
-            p.flags = (unsigned*)w;
-            p.err = (unsigned*)(w + fz.flag_bytes - 256);
-            p.part = (float*)(w + fz.flag_bytes);
-            p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
-            p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
-            // mode 3 (tests): the timeout word starts set, so every poll gives up
-            // and the guarded dQ pass must recompute dQ
-            if ((e = hipMemsetAsync(w, 0, fz.flag_bytes, s)) != hipSuccess ||
-                (g_bwd_mode == 3 && (e = hipMemsetAsync(p.err, 1, 4, s)) != hipSuccess)) {
-                *why = hipGetErrorString(e);
-                return FA_ERR_HIP;
-            }
+        if (fz.on && (size_t)(w - (char*)a.workspace) + fz.bytes <= a.workspace_bytes &&
+            (e = fused_setup(p, fz, w, s)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
         }
     }
     switch (a.dtype) {

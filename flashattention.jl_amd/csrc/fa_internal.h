@@ -93,6 +93,8 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why);
 size_t dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 size_t dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch);
 int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why);
+int dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes, hipStream_t s, int* status,
+                             const char** why);
 // Float64 (fa_f64.hip): the forward, and the backward's row statistics in double
 // (nD = −rowsum(dO ∘ O), nlse = −(m + ln l)/τ recomputed from Q, K; [batch][N] each)
 int launch_dense_fwd_f64(const DenseArgs& a, hipStream_t s, const char** why);

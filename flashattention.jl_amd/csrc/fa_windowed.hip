@@ -928,7 +928,9 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
 // --------------------------------------------------------------------------
 // NW (2 or 4) horizontally adjacent windows per workgroup staged by LDS-DMA
 // (bf16/f16, 2-D, stride >= ws, ws <= 7, d, dv <= 64, width % 8 == 0, 16-B
-// aligned).  The default forward.
+// aligned).  An experimental LDS-DMA variant, NOT the default (the default is
+// win_rows1s<..., 2>): the dispatcher launches it only under debug modes 7 / 8 of
+// fa_debug_set_win_composed, and it measured no faster.
 //
 // Slots are ROTATED instead of shifted: slot (yy, sx) of window w holds pixel
 // (ax + sx, y0 + yy) with ax = clamp(xs & ~1, 0, W - 8) the dword-aligned start

@@ -37,7 +37,7 @@ import torch
 __all__ = [
     "DimensionMismatch", "FlashAttentionError", "lib", "lib_path",
     "jl_empty", "jl_zeros", "jl_tensor", "jl_strides", "is_jl_contiguous",
-    "dense_fa", "dense_fa_", "dense_fa_backward", "windowed_fa", "block_fa",
+    "dense_fa", "dense_fa_", "dense_fa_backward", "backward_handoff_status", "windowed_fa", "block_fa",
     "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_", "circulant_dpa",
     "fused_softmax", "fused_softmax_", "DTYPES",
 ]
@@ -98,6 +98,8 @@ def lib() -> ctypes.CDLL:
     L.fa_dense_bwd.restype = ctypes.c_int
     L.fa_dense_bwd.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                i64, i64, i64, i64, i64, f32, vp, ctypes.c_size_t, vp]
+    L.fa_dense_bwd_handoff_status.restype = ctypes.c_int
+    L.fa_dense_bwd_handoff_status.argtypes = [vp, ctypes.c_size_t, vp, ctypes.POINTER(ctypes.c_int)]
     L.fa_windowed_workspace.restype = ctypes.c_size_t
     L.fa_windowed_workspace.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64),
                                         i64, i64, i64, i64, i64, i64]
@@ -384,6 +386,24 @@ def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
                           _ptr(dQ), _ptr(dK), _ptr(dV), N, Nk, d, dv, B, float(scale),
                           _ptr(ws), int(nws), _stream(Q)))
     return dQ, dK, dV
+
+
+def backward_handoff_status(device=None) -> int:
+    """fa_dense_bwd_handoff_status for the most recent :func:`dense_fa_backward`
+    on the current stream of ``device`` (its workspace is this module's per-stream
+    scratch buffer).  Synchronises that stream.  -1: the two-pass form ran (no
+    hand-off); 0: single pass, every dQ hand-off completed; 1: a hand-off timed out
+    and dQ was recomputed by the guarded pass (same values within rounding, other
+    bits, up to ~20 ms slower).  Raises FlashAttentionError when another entry point
+    has used the scratch buffer since."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    stream = torch.cuda.current_stream(device)
+    buf = _WS.get((device.type, device.index, stream.cuda_stream))
+    _require(buf is not None, "no backward has run on this stream")
+    st = ctypes.c_int(-2)
+    _check(lib().fa_dense_bwd_handoff_status(_ptr(buf), buf.numel(), ctypes.c_void_p(stream.cuda_stream),
+                                             ctypes.byref(st)))
+    return int(st.value)
 
 
 # ----------------------------------------------------------------------------

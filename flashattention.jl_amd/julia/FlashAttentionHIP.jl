@@ -72,9 +72,13 @@ function dense_fa(q::ROCArray{T,D}, k::ROCArray{T,D}, v::ROCArray{T,D}) where {T
 end
 
 # dense_fa_backward(Q, K, V, O, dO, l, m) — src/dense.jl:104-167
+# `handoff`: optional Ref{Cint} that receives fa_dense_bwd_handoff_status after the call
+# (-1 two-pass form, 0 single pass completed, 1 a dQ hand-off timed out and dQ was
+# recomputed); it synchronises the stream.
 function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
                            O::ROCArray{T,3}, dO::ROCArray{T,3},
-                           l::ROCArray{Float32,3}, m::ROCArray{Float32,3}) where {T}
+                           l::ROCArray{Float32,3}, m::ROCArray{Float32,3};
+                           handoff::Union{Nothing,Base.RefValue{Cint}}=nothing) where {T}
     N, d, B = size(Q)
     Nk, dv = size(K, 1), size(V, 2)
     size(K) == (Nk, d, B) && size(V) == (Nk, dv, B) ||
@@ -93,6 +97,10 @@ function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
                     Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
                    fa_dtype(T), Q, K, V, O, dO, l, m, dQ, dK, dV, N, Nk, d, dv, B, 0f0,
                    ws, nws, stream_ptr()))
+    if handoff !== nothing
+        fa_check(ccall((:fa_dense_bwd_handoff_status, libfa_hip), Cint,
+                       (Ptr{Cvoid}, Csize_t, Ptr{Cvoid}, Ptr{Cint}), ws, nws, stream_ptr(), handoff))
+    end
     return dQ, dK, dV
 end
 

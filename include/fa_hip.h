@@ -90,11 +90,14 @@ size_t fa_dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
                               int64_t dv, int64_t batch);
 
 /* Workspace bytes fa_dense_bwd needs for these sizes (0 is a valid answer):
- * 8·N·batch bytes of row statistics; for bf16 / fp16 shapes outside the MFMA
- * kernels' set, zero-padded copies; and when the single-pass kernel applies
- * (grids that fill the chip), per-slice counters plus the
- * running fp32 dQ sums, 4·N·d·batch bytes.  A smaller workspace that still
- * holds the first parts runs the two-pass form instead. */
+ * a 256-B header (fa_dense_bwd_handoff_status), 8·N·batch bytes of row
+ * statistics; for bf16 / fp16 shapes outside the MFMA kernels' set, zero-padded
+ * copies; and when the single-pass kernel applies (grids that
+ * fill the chip), per-slice counters plus the running fp32 dQ sums,
+ * 4·N·d·batch bytes (8.6 GB for configs[4]'s 1024 slabs of (16384, 128)).  A
+ * smaller workspace that still holds the first parts (the size this function
+ * returns under fa_debug_set_bwd_mode(1)) runs the two-pass form instead.  The
+ * answer depends on the current device's CU count. */
 size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
                               int64_t dv, int64_t batch);
 
@@ -103,8 +106,14 @@ size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
  * src_cpp/FlashAttention.cpp:194-252):
  *   P = exp(s - m)/l, dV = P^T dO, dP = dO V^T, D = rowsum(dO .* O),
  *   dS = P .* (dP - D), dQ = scale dS K, dK = scale dS^T Q.
- * l, m are the forward's outputs.  dQ, dK, dV are fully written and bitwise
- * reproducible (no atomics; the single pass sums dQ in a fixed order). */
+ * l, m are the forward's outputs.  dQ, dK, dV are fully written, without
+ * atomics.  dK and dV are bitwise reproducible.  dQ is bitwise reproducible
+ * whenever the single pass's ordered dQ hand-off completes (it sums each query
+ * slice over the key blocks in a fixed order); if a hand-off wait times out
+ * (20 ms: the members of a slab could not all be resident, e.g. other streams
+ * or processes holding CUs), dQ is recomputed by a separate pass that sums in a
+ * different order — same values within rounding, not the same bits, and up to
+ * ~20 ms slower.  fa_dense_bwd_handoff_status reports which happened. */
 int fa_dense_bwd(int dtype,
                  const void* Q, const void* K, const void* V,
                  const void* O, const void* dO,
@@ -113,6 +122,15 @@ int fa_dense_bwd(int dtype,
                  int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
                  float scale, void* workspace, size_t workspace_bytes,
                  void* hip_stream);
+
+/* Diagnostic for the call that last used `workspace` in fa_dense_bwd: reads the
+ * workspace header (synchronises hip_stream, so call it after that backward on the
+ * same stream).  *status = -1: that call ran the two-pass form (no hand-off),
+ * 0: single pass, every dQ hand-off completed, 1: single pass, a hand-off timed out
+ * and dQ was recomputed (see fa_dense_bwd).  FA_ERR_INVALID_ARG if the workspace
+ * holds no fa_dense_bwd header. */
+int fa_dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes,
+                                void* hip_stream, int* status);
 
 /* Windowed forward.  Replaces windowed_fa(q, k, v, ws; stride, pad)
  * (src/windowed.jl:3-23; block_fa = stride ws, src/windowed.jl:1), fusing

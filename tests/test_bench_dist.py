@@ -9,6 +9,8 @@ from __future__ import annotations
 import json
 import os
 import socket
+import subprocess
+import sys
 import time
 
 import numpy as np
@@ -81,5 +83,54 @@ def test_bench_strong_scaling_plumbing_two_ranks():
 def test_cpu_threads_respects_share(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
     assert bench._cpu_threads() == min(3, len(os.sched_getaffinity(0)))
+    assert bench._node_cpus() == len(os.sched_getaffinity(0))     # the node leg ignores the share
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert bench._cpu_threads() == len(os.sched_getaffinity(0))
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(FA_BENCH_CPU_STEP="1", FA_BENCH_BACKEND="gloo", OMP_NUM_THREADS="1", **extra)
+    return env
+
+
+def test_bench_gpus_2_literal_command_spawns_two_ranks():
+    """The driver's literal form `python bench.py --gpus 2` (no torch.distributed.run
+    around it) starts two ranks itself; with the CPU step hook (rank r sleeps
+    (r + 1) * 5 ms per step) the JSON line must say n_gpus 2, split configs[4]'s 1024
+    slabs as [[0, 512], [512, 1024]] and report the MAX over ranks (the slow rank)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+                        "--warmup", "1", "--cfg4-steps", "2", "--no-cpu"],
+                       cwd=ROOT, env=_bench_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    out = json.loads(lines[0])
+    assert out["cpu_step_hook"] is True
+    assert out["n_gpus"] == 2 and out["config"]["global_batch_heads"] == 128
+    assert out["config"]["parallelism"].startswith("shard(B*H) x2")
+    # MAX over ranks: rank 1's 10 ms per step, not rank 0's 5 ms
+    assert out["ms_per_step"] >= 10.0
+    c4 = out["cfg4"]
+    assert c4["n_gpus"] == 2 and c4["slab_split"] == [[0, 512], [512, 1024]]
+    assert c4["slabs_this_rank"] == 512 and c4["ms_per_step_max_over_ranks"] >= 10.0
+    assert abs(c4["tflops_per_gpu"] * 2 - c4["tflops_total"]) < 1e-9 * c4["tflops_total"]
+    # aggregate over both ranks: value = world * per-rank FLOPs / the slowest rank's time
+    flops_rank = 4.0 * 64 * 4096 * 4096 * 64
+    assert abs(out["value"] - 2 * flops_rank * 4 / (out["ms_per_step"] * 4 / 1e3) / 1e12) < 1e-6 * out["value"]
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    """Under torch.distributed.run, --gpus must equal WORLD_SIZE (exit 2), and
+    --gpus < 1 is refused, before anything is measured."""
+    env = _bench_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0"],
+                       cwd=ROOT, env=_bench_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2

@@ -45,7 +45,10 @@ def _worker(rank, world, port, out):
         jl = lambda a: torch.tensor(a).permute(2, 1, 0).contiguous().permute(2, 1, 0)
         Q, K, V = jl(q), jl(k), jl(v)
         lq, lk, lv = (local_slabs(t, world, rank) for t in (Q, K, V))
-        assert lq.is_contiguous() is False or True      # view of a column-major array
+        a, b = shard_range(BH, world, rank)
+        # a zero-copy view: the rank's slabs are one contiguous byte range of the global array
+        assert lq.data_ptr() == Q.data_ptr() + a * N * d * Q.element_size()
+        assert lq.shape == (N, d, b - a) and lq.stride() == Q.stride()
         y, l, m = O.dense_fa3(lq.numpy(), lk.numpy(), lv.numpy())   # per-rank compute, no collective
         yl = jl(y)
         full = gather_slabs(yl, BH)

@@ -209,15 +209,27 @@ def test_backward_f32_mfma_path(fa, N, Nk, d, dv):
         assert_grad_close(_np(a), _np(g_), "float32", nm + " vs generic")
 
 
-def _bwd_mode(fa, mode, *args):
+def _bwd_mode(fa, mode, *args, status=None):
     L = fa.lib()
     old = L.fa_debug_set_bwd_mode(mode)
+    assert old >= 0
     try:
         out = fa.dense_fa_backward(*args)
         torch.cuda.synchronize()
+        if status is not None:
+            status.append(fa.backward_handoff_status())
     finally:
         L.fa_debug_set_bwd_mode(old)
     return out
+
+
+def test_bwd_mode_knob_rejects_ablations(fa):
+    """The timing-only ablation modes (wrong dQ) are compiled out of the shipped
+    library: the knob refuses them and keeps the current mode."""
+    L = fa.lib()
+    for bad in (4, 5, 6, 7, 8, 9, 10, -1):
+        assert L.fa_debug_set_bwd_mode(bad) == -1
+    assert L.fa_debug_set_bwd_mode(0) == 0
 
 
 @pytest.mark.parametrize("N,Nk,d,dv,B", [(512, 512, 64, 64, 2), (1024, 1024, 128, 128, 2), (1000, 520, 128, 64, 3),
@@ -235,9 +247,12 @@ def test_backward_single_pass(fa, N, Nk, d, dv, B, dtype):
     v, do = cast(rng.standard_normal((Nk, dv, B))), cast(rng.standard_normal((N, dv, B)))
     Q, K, V, dO = (fa.jl_tensor(a, tdt) for a in (q, k, v, do))
     Oo, l, m = fa.dense_fa(Q, K, V)
-    one = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m)
-    again = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m)
-    split = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m)
+    st = []
+    one = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m, status=st)
+    again = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m, status=st)
+    split = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m, status=st)
+    # the padded (513, 300, 40, 24) case runs the single pass on the padded shape too
+    assert st == [0, 0, -1], st
     dqr, dkr, dvr = O.dense_fa_backward(q, k, v, _np(Oo), do, _np(l), _np(m))
     for a, a2, sp, r_, nm in zip(one, again, split, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
         assert torch.equal(a, a2), nm + " not reproducible"
@@ -252,7 +267,60 @@ def test_backward_single_pass_fallback(fa):
     N, d, B = 1024, 128, 2
     Q, K, V, dO = (fa.jl_tensor(rng.standard_normal((N, d, B)), torch.bfloat16) for _ in range(4))
     Oo, l, m = fa.dense_fa(Q, K, V)
-    fb = _bwd_mode(fa, 3, Q, K, V, Oo, dO, l, m)
-    sp = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m)
+    st = []
+    fb = _bwd_mode(fa, 3, Q, K, V, Oo, dO, l, m, status=st)
+    sp = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m, status=st)
+    assert st == [1, -1], st          # the timeout is reported
     for a, b_, nm in zip(fb, sp, ("dQ", "dK", "dV")):
         assert_grad_close(_np(a), _np(b_), "bfloat16", nm + " (fallback) vs split passes")
+
+
+def test_backward_handoff_status_errors(fa):
+    """The status query refuses a workspace that no backward wrote a header into."""
+    rng = np.random.default_rng(2)
+    Q, K, V = (fa.jl_tensor(rng.standard_normal((256, 64, 2)), torch.bfloat16) for _ in range(3))
+    fa.windowed_fa(fa.jl_tensor(rng.standard_normal((16, 16, 64, 1)), torch.bfloat16),
+                   fa.jl_tensor(rng.standard_normal((16, 16, 64, 1)), torch.bfloat16),
+                   fa.jl_tensor(rng.standard_normal((16, 16, 64, 1)), torch.bfloat16), 4)
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    fa.dense_fa_backward(Q, K, V, Oo, Oo, l, m)
+    assert fa.backward_handoff_status() in (-1, 0)
+    L = fa.lib()
+    junk = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    st = __import__("ctypes").c_int(5)
+    rc = L.fa_dense_bwd_handoff_status(fa._ptr(junk), 1024, None, __import__("ctypes").byref(st))
+    assert rc == fa.FA_ERR_INVALID_ARG and st.value == 5
+
+
+def test_backward_two_streams_concurrent(fa):
+    """Two configs[3]-sized backward calls (N 8192, d 128, 64 slabs) on two streams at
+    once: each single pass needs all 32 members of a slab resident, and the other
+    stream holds CUs.  Both results match the float64 oracle on one slab each; the
+    hand-off status of each call is reported (a timeout is correct but slow)."""
+    N, d, BH = 8192, 128, 64
+    g = torch.Generator(device="cuda").manual_seed(23)
+    mk = lambda: fa.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
+    ins = []
+    for _ in range(2):
+        Q, K, V, dO = mk(), mk(), mk(), mk()
+        Oo, l, m = fa.dense_fa(Q, K, V)
+        ins.append((Q, K, V, Oo, dO, l, m))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs, status = [None, None], [None, None]
+    for i in range(2):
+        with torch.cuda.stream(streams[i]):
+            outs[i] = fa.dense_fa_backward(*ins[i])
+    for i in range(2):
+        with torch.cuda.stream(streams[i]):
+            status[i] = fa.backward_handoff_status()
+    torch.cuda.synchronize()
+    print(f"two-stream backward hand-off status: {status}")
+    assert all(s in (-1, 0, 1) for s in status)
+    for i, b in ((0, 5), (1, 40)):
+        Q, K, V, Oo, dO, l, m = ins[i]
+        sl = lambda t: _np(t[:, :, b:b + 1])
+        dqr, dkr, dvr = O.dense_fa_backward(sl(Q), sl(K), sl(V), sl(Oo), sl(dO),
+                                            _np(l[:, :, b:b + 1]), _np(m[:, :, b:b + 1]))
+        for a, r_, nm in zip(outs[i], (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+            assert_grad_close(sl(a), r_, "bfloat16", f"stream {i} {nm}")

@@ -14,7 +14,7 @@ HDR = os.path.join(ROOT, "include", "fa_hip.h")
 
 C2JL = {"int": "Cint", "int64_t": "Int64", "size_t": "Csize_t", "float": "Cfloat",
         "void*": "Ptr{Cvoid}", "float*": "Ptr{Float32}", "int64_t*": "Ptr{Int64}",
-        "char*": "Cstring", "void": "()"}
+        "char*": "Cstring", "int*": "Ptr{Cint}", "void": "()"}
 
 
 def _norm_c(t: str) -> str:
