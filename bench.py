@@ -380,13 +380,39 @@ def _node_cpus():
     return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
 
 
-def cpu_baseline():
+def _plain_port(Q, K, V, nthreads):
+    """oracle/fa_cpu.c's OpenMP port of dense_fa! without BLAS (same tiles, scalar
+    / SIMD loops), for thread counts past numpy's OpenBLAS build limit."""
+    import ctypes
+    import numpy as np
+    from oracle import cpu_port
+    N, d, B = Q.shape
+    O = np.empty((N, V.shape[1], B), np.float32, order="F")
+    l = np.empty((N, 1, B), np.float32, order="F")
+    m = np.empty((N, 1, B), np.float32, order="F")
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    rc = cpu_port.lib().fa_cpu_dense_fwd_f32(p(Q), p(K), p(V), p(O), p(l), p(m), N, K.shape[0], d, V.shape[1], B,
+                                             int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"fa_cpu_dense_fwd_f32 failed ({rc})")
+    return O
+
+
+# numpy's OpenBLAS is built with MAX_THREADS=64: more concurrent single-threaded sgemm
+# callers than its buffer table holds corrupt its allocator ("Bad memory unallocation")
+OPENBLAS_MAX_CALLERS = 64
+
+
+def cpu_baseline(node: bool = False):
     """The reference's CPU algorithm, dense_fa! (src/dense.jl:21-102), as the
     BLAS-backed C/OpenMP port oracle/fa_cpu.c (same Br/Bc tiles, one gemm per
-    tile product, (slab x row-block) tasks), fp32, at two thread counts:
-      * "node": every CPU of the process's affinity set (the node's host cores,
-        north_star) -> `value` / `cores`;
-      * "share": the box's per-GPU OMP_NUM_THREADS share (16 on the GPU box).
+    tile product, (slab x row-block) tasks), fp32.
+      * default leg "share": the box's per-GPU OMP_NUM_THREADS share (16 on the GPU
+        box; the harness asks GPU jobs to keep their worker pools to it) -> `value`;
+      * node=True (bench.py --cpu-node) adds the node's host cores, every CPU of the
+        affinity set (north_star): "node_blas" = the BLAS port at min(CPUs, 64)
+        threads (numpy's OpenBLAS build limit), "node_plain" = the same algorithm
+        without BLAS on all CPUs; `value` / `cores` then come from the faster leg.
     Each leg times configs[0] (N,d,B·H) = (512,64,4) (median of 50 after 5
     warm-ups; also at 1 thread), the reference's own published Float64 case
     (512,64,1) (logs/compare1.txt:4), and the whole configs[1] workload
@@ -394,7 +420,7 @@ def cpu_baseline():
     import numpy as np
     from oracle import cpu_port
     cpu_port.blas_info()
-    node, share = _node_cpus(), _cpu_threads()
+    ncpu, share = _node_cpus(), _cpu_threads()
     rng = np.random.default_rng(0)
 
     def arrs(N, d, n, dt=np.float32):
@@ -415,26 +441,33 @@ def cpu_baseline():
     q1, k1, v1 = arrs(N_, D_, B_ * H_)
     f0, fr, f1 = 4.0 * 4 * 512 * 512 * 64, 4.0 * 512 * 512 * 64, 4.0 * B_ * H_ * N_ * N_ * D_
     legs = {}
-    for tag, th in (("node", node), ("share", share)):
-        if tag == "share" and share == node:
-            legs[tag] = "same thread count as the node leg"
-            continue
+    plan = [("share", share, "blas")]
+    if node:
+        plan += [("node_blas", min(ncpu, OPENBLAS_MAX_CALLERS), "blas"), ("node_plain", ncpu, "plain")]
+    for tag, th, kind in plan:
+        run = (lambda q, k, v, t_: cpu_port.dense_fa_blas(q, k, v, t_)) if kind == "blas" else _plain_port
         c0 = {}
         for t_ in sorted({1, th}):
-            t = med_time(lambda: cpu_port.dense_fa_blas(q0, k0, v0, t_), 50, 5)
+            t = med_time(lambda: run(q0, k0, v0, t_), 50, 5)
             c0[f"threads_{t_}"] = {"ms": t * 1e3, "gflops": f0 / t / 1e9}
-        tr = med_time(lambda: cpu_port.dense_fa_blas(qr, kr, vr, th), 50, 5)
-        t1 = med_time(lambda: cpu_port.dense_fa_blas(q1, k1, v1, th), 3, 1)
-        legs[tag] = {"threads": th, "configs1_fp32_tflops": f1 / t1 / 1e12, "configs1_s": t1,
-                     "configs0_fp32_512x64x4": c0,
-                     "reference_case_f64_512x64x1": {"ms": tr * 1e3, "gflops": fr / tr / 1e9}}
-    nl = legs["node"]
-    return {"value": nl["configs1_fp32_tflops"], "unit": "TFLOP/s", "cores": node, "kind": "port",
-            "cpu_model": _cpu_model(), "affinity_cpus": node, "omp_share": share,
-            "sample": f"the whole configs[1] workload (4096,64,64) fp32, BLAS-backed C/OpenMP port of dense_fa! "
-                      f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles, OpenBLAS sgemm per tile product) on all {node} "
-                      f"affinity CPUs, median of 3: {nl['configs1_s']:.3f} s; 'legs' adds the per-GPU "
-                      f"{share}-thread share, configs[0] and the reference's Float64 case",
+        leg = {"threads": th, "impl": "BLAS port (OpenBLAS sgemm per tile product)" if kind == "blas"
+               else "OpenMP port without BLAS", "configs0_fp32_512x64x4": c0}
+        if kind == "blas":
+            tr = med_time(lambda: cpu_port.dense_fa_blas(qr, kr, vr, th), 50, 5)
+            leg["reference_case_f64_512x64x1"] = {"ms": tr * 1e3, "gflops": fr / tr / 1e9}
+        t1 = med_time(lambda: run(q1, k1, v1, th), 3, 1)
+        leg.update(configs1_fp32_tflops=f1 / t1 / 1e12, configs1_s=t1)
+        legs[tag] = leg
+    best = max(legs, key=lambda t: legs[t]["configs1_fp32_tflops"])
+    bl = legs[best]
+    return {"value": bl["configs1_fp32_tflops"], "unit": "TFLOP/s", "cores": bl["threads"], "kind": "port",
+            "value_from": best, "cpu_model": _cpu_model(), "affinity_cpus": ncpu, "omp_share": share,
+            "sample": f"the whole configs[1] workload (4096,64,64) fp32, C/OpenMP port of dense_fa! "
+                      f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles), leg '{best}': {bl['impl']} at {bl['threads']} "
+                      f"threads, median of 3: {bl['configs1_s']:.3f} s; 'legs' adds configs[0] and the "
+                      f"reference's Float64 case" + ("" if node else
+                      f"; the node-wide legs (all {ncpu} CPUs) run with bench.py --cpu-node "
+                      f"(profiles/r03_cpu_baseline_node.log)"),
             "legs": legs,
             "reference_published": "dense_fa Julia N=512 d=64 bs=1 Float64: 2.392 ms, unstated CPU "
                                    "(/root/reference/logs/compare1.txt:4)"}
@@ -490,6 +523,8 @@ def main():
                     help="untimed back-to-back launches before timing (disclosed in the JSON)")
     ap.add_argument("--cfg4-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-node", action="store_true",
+                    help="cpu_baseline also on every affinity CPU (beyond the box's per-GPU share)")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the configs[4] strong-scaling block")
     ap.add_argument("--no-cfg23", action="store_true", help="skip the configs[2] / configs[3] blocks")
     ap.add_argument("--extra", action="store_true", help="also time the secondary paths (reported under 'extra')")
@@ -578,7 +613,7 @@ def main():
         out["extra"] = extra_benches(fa_hip, args, dist)
 
     if rank == 0 and world == 1 and not args.no_cpu and not cpu_hook:
-        out["cpu_baseline"] = cpu_baseline()
+        out["cpu_baseline"] = cpu_baseline(node=args.cpu_node)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -47,6 +47,17 @@
 #include "fa_fwd_params.h"
 #include "../../include/fa_hip.h"
 
+// Diagnostic hooks (tools/exp/fwd_stamp.hip; empty / 0 in the product build):
+// FA_FWD_STAMP(k) records s_memtime / s_memrealtime at phase k of dense_fwd_tiled;
+// FA_FWD_ABL selects timing-only ablations that compute WRONG results
+// (1: no v_exp, 2: no row sum, 4: no row max).
+#ifndef FA_FWD_STAMP
+#define FA_FWD_STAMP(k)
+#endif
+#ifndef FA_FWD_ABL
+#define FA_FWD_ABL 0
+#endif
+
 namespace fa {
 
 thread_local int g_fwd_variant = 0;  // 0: auto; 4..7: forced geometry (benchmark knob, fa_debug_set_fwd_variant)
@@ -486,6 +497,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
     // f+1 are 32 banks apart already; 256-B rows need a 2-bit XOR).
     auto kswz = [](int f) { return BN == 64 ? (((f >> 1) & 1) << 1) : ((f & 3) << 1); };
 
+    FA_FWD_STAMP(0);
     int lid = xcd_remap(blockIdx.x, p.total_wg);
     const int split = SPLIT ? lid % p.nsplit : 0;
     if (SPLIT) lid /= p.nsplit;
@@ -623,7 +635,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         F8 pf[NQB][NKB][2];
 #pragma unroll
         for (int u = 0; u < NQB; ++u) {
-            const float mt = swap_halves_max(lane_max<NKB>(sacc[u]));
+            const float mt = (FA_FWD_ABL & 4) ? sacc[u][0][0] : swap_halves_max(lane_max<NKB>(sacc[u]));
             m_true[u] = vmax(m_true[u], mt);
             if (__builtin_amdgcn_ballot_w64(mt > m_used[u] + thr_raw) != 0) {
                 const float m_new = fmaxf(m_used[u], mt);
@@ -641,10 +653,11 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
                 for (int x = 0; x < 16; ++x) {
-                    const float pv = exp2_fast(fmaf(sacc[u][kb][x], c, -mc));
+                    const float arg = fmaf(sacc[u][kb][x], c, -mc);
+                    const float pv = (FA_FWD_ABL & 1) ? arg : exp2_fast(arg);
                     // first four seed the partial sums (no `0 + p` adds: without
                     // fast-math the compiler must keep them, -0 + 0 != -0)
-                    if (kb == 0 && x < 4) ps[x] = pv; else ps[x & 3] += pv;
+                    if (kb == 0 && x < 4) ps[x] = pv; else if (!(FA_FWD_ABL & 2)) ps[x & 3] += pv;
                     pf[u][kb][x >> 3][x & 7] = (T)pv;
                 }
             l_run[u] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
@@ -680,6 +693,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
                 qf[u][s] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
             }
     }
+    FA_FWD_STAMP(1);
     for (int j = jt0; j < jt1; j += 2) {
         gload(min(j + 1, jt1 - 1));
         compute(buf0, buf0 + KBYTES, j);
@@ -692,6 +706,7 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
             __syncthreads();
         }
     }
+    FA_FWD_STAMP(2);
 
     if constexpr (SPLIT) {   // partials: O, l relative to exp2(c (s - m_true)), m_true in raw units
         const int64_t sb = (int64_t)split * p.batch + b;
@@ -745,8 +760,12 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
             const int ch = it * NTH + tid, f = ch / CPRO, lb = (ch - f * CPRO) * 16;
             const int q = qb * BM + lb / 2;
             const u32x4 v4 = *(const u32x4*)(qoimg + qo_at(f, lb));
-            if (f < dv && q < N) __builtin_amdgcn_raw_buffer_store_b128(v4, ors, (f * N + q) * 2, 0, 0);
+            // branch-free: a chunk outside (dv, N) gets an offset past the slab descriptor's
+            // range, which the buffer store drops (no per-store exec-mask branch in the tail)
+            const int off = (f < dv && q < N) ? (f * N + q) * 2 : 0x7FFFFFF0;
+            __builtin_amdgcn_raw_buffer_store_b128(v4, ors, off, 0, 0);
         }
+        FA_FWD_STAMP(3);
         return;
     }
 #pragma unroll

@@ -83,7 +83,7 @@ def test_bench_strong_scaling_plumbing_two_ranks():
 def test_cpu_threads_respects_share(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
     assert bench._cpu_threads() == min(3, len(os.sched_getaffinity(0)))
-    assert bench._node_cpus() == len(os.sched_getaffinity(0))     # the node leg ignores the share
+    assert bench._node_cpus() == len(os.sched_getaffinity(0))     # the node legs ignore the share
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert bench._cpu_threads() == len(os.sched_getaffinity(0))
 
@@ -134,3 +134,25 @@ def test_bench_refuses_gpus_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0"],
                        cwd=ROOT, env=_bench_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 2
+
+
+def test_cpu_baseline_legs_small(monkeypatch):
+    """cpu_baseline's legs on a reduced workload (CPU): the BLAS port and the plain
+    OpenMP port agree with each other, and the node legs cap the BLAS callers at
+    numpy's OpenBLAS limit."""
+    import numpy as np
+    monkeypatch.setattr(bench, "N_", 256)
+    monkeypatch.setattr(bench, "B_", 1)
+    monkeypatch.setattr(bench, "H_", 2)
+    monkeypatch.setattr(bench, "_node_cpus", lambda: 2)
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    out = bench.cpu_baseline(node=True)
+    assert set(out["legs"]) == {"share", "node_blas", "node_plain"}
+    assert out["legs"]["node_blas"]["threads"] == min(2, bench.OPENBLAS_MAX_CALLERS)
+    assert out["value"] > 0 and out["cores"] in (1, 2)
+    from oracle import cpu_port
+    rng = np.random.default_rng(1)
+    q, k, v = (np.asfortranarray(rng.standard_normal((96, 16, 2)).astype(np.float32)) for _ in range(3))
+    a = cpu_port.dense_fa_blas(q, k, v, 2)[0]
+    b = bench._plain_port(q, k, v, 2)
+    assert np.abs(a - b).max() < 1e-5
