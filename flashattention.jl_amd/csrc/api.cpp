@@ -157,10 +157,10 @@ int fa_debug_set_circ_generic(int v) {
 // 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window
 // row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the auto choice at ws <= 7),
 // 7 / 8 two- / four-window LDS-DMA with rotated slots, 9 segment-owning (16-B y stores),
-// where eligible; 0 auto).
+// 10 eight-window strip (stride == ws), where eligible; 0 auto).
 int fa_debug_set_win_composed(int v) {
     const int old = fa::g_win_force_composed;
-    fa::g_win_force_composed = (v >= 1 && v <= 9) ? v : 0;
+    fa::g_win_force_composed = (v >= 1 && v <= 10) ? v : 0;
     return old;
 }
 

@@ -635,10 +635,14 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         F8 pf[NQB][NKB][2];
 #pragma unroll
         for (int u = 0; u < NQB; ++u) {
-            const float mt = (FA_FWD_ABL & 4) ? sacc[u][0][0] : swap_halves_max(lane_max<NKB>(sacc[u]));
+            // lane-local tile max (this lane's half of the keys): the lazy check needs no
+            // cross-lane step, since the query's other half-lane takes part in the same
+            // wave-wide ballot; only a rescale combines the halves.  m_true stays
+            // lane-local and is combined once after the loop (bitwise the same result).
+            const float mt = (FA_FWD_ABL & 4) ? sacc[u][0][0] : lane_max<NKB>(sacc[u]);
             m_true[u] = vmax(m_true[u], mt);
             if (__builtin_amdgcn_ballot_w64(mt > m_used[u] + thr_raw) != 0) {
-                const float m_new = fmaxf(m_used[u], mt);
+                const float m_new = fmaxf(m_used[u], swap_halves_max(mt));
                 const float alpha = exp2_fast((m_used[u] - m_new) * c);
                 l_run[u] *= alpha;
 #pragma unroll
@@ -707,6 +711,8 @@ __device__ __forceinline__ void dense_fwd_tiled(const FwdParams& p) {
         }
     }
     FA_FWD_STAMP(2);
+#pragma unroll
+    for (int u = 0; u < NQB; ++u) m_true[u] = swap_halves_max(m_true[u]);   // the query's two half-lanes
 
     if constexpr (SPLIT) {   // partials: O, l relative to exp2(c (s - m_true)), m_true in raw units
         const int64_t sb = (int64_t)split * p.batch + b;
@@ -1005,10 +1011,12 @@ __device__ __forceinline__ void dense_fwd_t16(const FwdParams& p) {
             float a2 = vmax3(s[1][2], s[1][3], s[2][0]), a3 = vmax3(s[2][1], s[2][2], s[2][3]);
             a0 = vmax3(a0, s[3][0], s[3][1]);
             a1 = vmax3(a1, s[3][2], s[3][3]);
-            const float mt = swap_halves_max(swap16_max(vmax(vmax3(a0, a1, a2), a3)));
+            // lane-local tile max (a query's 64 keys sit on 4 lanes): the lazy check is a
+            // wave-wide ballot, so only a rescale needs the 4-lane max (see dense_fwd_tiled)
+            const float mt = vmax(vmax3(a0, a1, a2), a3);
             m_true[u] = vmax(m_true[u], mt);
             if (__builtin_amdgcn_ballot_w64(mt > m_used[u] + thr_raw) != 0) {
-                const float m_new = fmaxf(m_used[u], mt);
+                const float m_new = fmaxf(m_used[u], swap_halves_max(swap16_max(mt)));
                 const float alpha = exp2_fast((m_used[u] - m_new) * c);
                 l_run[u] *= alpha;
 #pragma unroll
@@ -1057,6 +1065,8 @@ __device__ __forceinline__ void dense_fwd_t16(const FwdParams& p) {
             __syncthreads();
         }
     }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) m_true[u] = swap_halves_max(swap16_max(m_true[u]));   // the query's 4 lanes
 
     if constexpr (SPLIT) {   // partials: O, l relative to exp2(c (s - m_true)), m_true in raw units
         const int64_t sb = (int64_t)split * p.batch + b;

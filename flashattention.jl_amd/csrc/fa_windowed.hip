@@ -30,7 +30,9 @@
 #define FA_STAMP(k)
 #endif
 // Timing-only ablations of win_rows1s (tools/exp/win_ablate.hip; 0 in the product):
-// 1 = no y stores, 2 = every row load from one address
+// 1 = no y stores, 2 = every row load from one address; of win_strip
+// (tools/exp/strip_stamp.py): 4 = no y strip-image writes, 8 = no y global stores,
+// 16 = no 2-B stores of the chunks shared with a neighbour strip
 #ifndef FA_WIN_ABL
 #define FA_WIN_ABL 0
 #endif
@@ -1176,6 +1178,275 @@ __global__ __launch_bounds__(256 * NW, 8) void win_dma(const T* __restrict__ q, 
 }
 
 // --------------------------------------------------------------------------
+// Strip kernel: NS = 8 horizontally adjacent windows of one window row per
+// workgroup, one window per wave (bf16/f16, 2-D, stride == ws <= 7, d, dv <= 64,
+// width % 8 == 0, q, k, v, y 16-B aligned; the default for large launches).
+//
+// Why: the per-window kernels move q, k, v and y in 14-B window-row segments, so
+// every load / store instruction touches ~64 cache lines that ~9 windows of other
+// workgroups share: ~14 M L2 requests of ~20 B per configs[2] B = 32 call
+// (r02_windowed_fwd_pmc.txt), which sets their pace, not HBM.  Here the eight
+// windows' rows sit side by side in every DMA instruction (8 lanes x 16 B per
+// cache line) and y leaves as whole 16-B chunks of the strip's 56 contiguous
+// pixels.  The first strip holds k0 <= 8 windows, k0 chosen so that every strip
+// boundary falls on a 16-B chunk boundary (k0 * ws = pad mod 8, solvable for odd
+// ws): then no chunk is shared with a neighbour strip.  When no k0 aligns them
+// (even ws), the two strip ends are 2-B stores.
+//
+// Channels are streamed so the eight windows fit in LDS:
+//   * two 32-KB buffers (64 KB: two workgroups per CU) take the image loads in
+//     turn, each issued as soon as its buffer is free: Q / K chunks of 16 features
+//     ([16 f][8 slot rows][8 windows] x 16 B, 16 KB each), then the two 32-feature
+//     V chunks ([32 f][8][8] x 16 B), which land under the last QKᵀ steps;
+//     Sᵀ = K·Qᵀ accumulates over the chunks (one 16-deep MFMA step per chunk,
+//     64 x 64 slots per window, 2 x 2 blocks);
+//   * y: per V chunk, each wave writes its window's normalised O into a strip
+//     image [32 f][8 rows][64 px] over that V chunk, then the workgroup stores it
+//     row by row.
+// Slots are ROTATED as in win_dma: slot (yy, sx) of window w holds pixel
+// (ax_w + sx, y0 + yy), ax_w = clamp(xs_w & ~1, 0, W - 8); padding columns enter
+// the softmax analytically (npad zero keys), padding rows load as zeros.
+// LDS-DMA writes lane-linearly, so the swizzles are applied through each lane's
+// choice of (window, slot row):
+//   Q / K: window position w ^ ((f & 3) | ((c >> 1) & 1) << 2)  (ds_read_b64_tr_b16, conflict-free);
+//   V    : slot-row position c ^ ((f >> 3) & 1), window position w ^ (f & 7)  (ds_read_b128, conflict-free).
+// --------------------------------------------------------------------------
+constexpr int kStripW = 8;                          // windows per strip workgroup
+__device__ __forceinline__ int sqk_pos(int f, int c, int w) {   // byte offset in a Q / K chunk image
+    return f * 1024 + c * 128 + ((w ^ ((f & 3) | (((c >> 1) & 1) << 2))) << 4);
+}
+__device__ __forceinline__ int sv_pos(int f, int c, int w) {    // byte offset in a V chunk image
+    return f * 1024 + ((c ^ ((f >> 3) & 1)) << 7) + ((w ^ (f & 7)) << 4);
+}
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, const T* __restrict__ k,
+                                                    const T* __restrict__ v, T* __restrict__ out,
+                                                    float* __restrict__ lo, float* __restrict__ mo, WinDev g, int d,
+                                                    int dv, int nsx, int k0, int nwg, float scale, float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    static_assert(D % 16 == 0 && D <= 64 && DV % 32 == 0 && DV <= 64, "head dims");
+    constexpr int NQC = D / 16, NVC = DV / 32;       // Q/K chunks of 16 features, V chunks of 32
+    constexpr int NLD = NQC + NVC;                   // image loads, alternating between the two buffers
+    constexpr int BUF = 32768;
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];   // 64 KB: two workgroups per CU
+
+    FA_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride, nwx = g.O[0];
+    const int lid = xcd_remap(blockIdx.x, nwg);
+    const int sxi = lid % nsx, t0 = lid / nsx, wy = t0 % g.O[1], b = t0 / g.O[1];
+    const int wx0 = sxi == 0 ? 0 : k0 + (sxi - 1) * kStripW, y0 = wy * st - g.pad;
+    const int nvalid = min(sxi == 0 ? k0 : kStripW, nwx - wx0);
+    auto ax_of = [&](int w) { return min(max(((wx0 + w) * st - g.pad) & ~1, 0), W_ - 8); };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+
+    // one DMA instruction = one feature row f of an image: lane -> (slot row, window).
+    // (buffer descriptors are passed, not captured: a lambda capturing one made
+    // hipcc's host pass drop the kernel's launch stub, with no diagnostic)
+    auto dma_qk = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg) {
+        const int pc = lane >> 3, pw = lane & 7;
+        const int w = pw ^ ((fl & 3) | (((pc >> 1) & 1) << 2)), y = y0 + pc;
+        const bool ok = w < nvalid && pc < ws && y >= 0 && y < H_ && fg < d;
+        const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
+                                                 off, 0, 0, 0);
+    };
+    auto dma_v = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg) {
+        const int c = (lane >> 3) ^ ((fl >> 3) & 1), w = (lane & 7) ^ (fl & 7), y = y0 + c;
+        const bool ok = w < nvalid && c < ws && y >= 0 && y < H_ && fg < dv;
+        const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
+                                                 off, 0, 0, 0);
+    };
+    // image load i (QK chunk i, then V chunk i - NQC) into buffer i & 1: 32 DMA
+    // instructions (one feature row each), 4 per wave
+    auto issue = [&](__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, int i) {
+        char* buf = smem + (i & 1) * BUF;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int rr = j * 8 + wave;                  // 0..31
+            if (i < NQC) {
+                if (rr < 16) dma_qk(qr, buf, rr, i * 16 + rr);
+                else dma_qk(kr, buf + 16384, rr - 16, i * 16 + rr - 16);
+            } else {
+                dma_v(vr, buf, rr, (i - NQC) * 32 + rr);
+            }
+        }
+    };
+    issue(qrs, krs, vrs, 0);
+    issue(qrs, krs, vrs, 1);
+
+    // ---- this wave's window ----
+    const int wl = wave;
+    const bool wok = wl < nvalid;
+    const int wx = wx0 + wl, xs = wx * st - g.pad, ax = ax_of(wl);
+    const int c0 = xs - ax, c1 = c0 + ws;
+    const int ncols = min(c1, 8) - max(c0, 0);
+    const float npad = (float)((ws - ncols) * ws);       // padding-column tokens (zero keys)
+    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+
+    f32x16 sa[2][2];                                     // [key block][query block]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sa[kb][qb][x] = 0.0f;
+
+    // Load cc is consumed at step cc; load cc + 1 is always the one issued after it,
+    // so this wave waits with 4 DMA instructions in flight, then an LDS-only barrier
+    // (a __syncthreads fence would drain those too) makes every wave's part visible.
+#pragma unroll
+    for (int cc = 0; cc < NQC; ++cc) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        lds_barrier();
+        if (cc == 0) FA_STAMP(1);
+        const char* buf = smem + (cc & 1) * BUF;
+        // tr-read rows 8h + qq (+4): chunk-local features; slot rows 4blk + 2kh + (sig >> 1) / qb*4 + 2kh + (pp >> 1)
+        F8 kf[2], qf[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+            const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
+            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
+                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 1024)), 0, 1, 2, 3, 4, 5, 6, 7);
+            const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
+            qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(aq)),
+                                              __builtin_bit_cast(F4, ds_read_tr16(aq + 4 * 1024)), 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) sa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], sa[kb][qb]);
+        if (cc + 2 < NLD) {
+            lds_barrier();                                // every wave is done with this buffer
+            issue(qrs, krs, vrs, cc + 2);
+        }
+    }
+
+    FA_STAMP(2);
+    // ---- exact softmax per query over the window's real keys (+ npad zero keys) ----
+    F8 pf[2][2][2];                                      // [query block][key block][16-key half]
+    float mt[2], lt[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+                const int sx = kt & 7;
+                if ((kt >> 3) >= ws || sx < c0 || sx >= c1) sa[kb][qb][x] = kNegInf;
+            }
+        f32x16 two[2] = {sa[0][qb], sa[1][qb]};
+        float m = swap_halves_max(lane_max<2>(two));
+        if (npad > 0.0f) m = vmax(m, 0.0f);
+        const float mc = m * scale_log2;
+        float ps[4];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = exp2_fast(fmaf(sa[kb][qb][x], scale_log2, -mc));
+                if (kb == 0 && x < 4) ps[x] = pr; else ps[x & 3] += pr;
+                pf[qb][kb][x >> 3][x & 7] = (T)pr;
+            }
+        float l = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
+        if (npad > 0.0f) l = fmaf(npad, exp2_fast(-mc), l);
+        mt[qb] = m;
+        lt[qb] = l;
+    }
+    // l, m (window layout) and the padding-column query tokens
+    if (wok) {
+        const int64_t wbase = (int64_t)g.T * ((int64_t)(wx + nwx * wy) + (int64_t)g.L * b);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            const int qs = qb * 32 + r, qtx = qs & 7, qty = qs >> 3;
+            if (h == 0 && qtx >= c0 && qtx < c1 && qty < ws) {
+                const int64_t li = wbase + qty * ws + (qtx - c0);
+                mo[li] = mt[qb] * scale;
+                lo[li] = lt[qb];
+            }
+        }
+        if (lane < g.T) {                                 // padding-column query tokens (q = 0): every score is 0
+            const int px = xs + lane % ws;
+            if (px < 0 || px >= W_) {
+                mo[wbase + lane] = 0.0f;
+                lo[wbase + lane] = (float)g.T;
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's V DMA (and the l, m stores)
+    lds_barrier();                                       // every wave's V landed
+    FA_STAMP(3);
+
+    // ---- per 32-feature chunk: Oᵀ = Vᵀ·Pᵀ, then (over the V image) the strip image
+    //      [32 f][8 rows][64 px] of normalised O, then 16-B stores of the strip's pixels ----
+    const int xs0 = wx0 * st - g.pad, X0 = xs0 & ~7;     // strip start, its 16-B aligned base
+    const int xlo = max(xs0, 0), xhi = min(xs0 + nvalid * ws, W_);
+    const auto ors = slab_rsrc(out + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    unsigned vm[4];                                      // key-slot mask of a V fragment (one slot row)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        vm[j] = ((2 * j >= c0 && 2 * j < c1) ? 0x0000FFFFu : 0u) | ((2 * j + 1 >= c0 && 2 * j + 1 < c1) ? 0xFFFF0000u : 0u);
+#pragma unroll
+    for (int vc = 0; vc < NVC; ++vc) {
+        char* img = smem + ((NQC + vc) & 1) * BUF;
+        f32x16 oa[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oa[qb][x] = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                u32x4 vr = *(const u32x4*)(img + sv_pos(r, kb * 4 + s2 * 2 + h, wl));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) vr[j] &= vm[j];
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) oa[qb] = mfma32x32x16(__builtin_bit_cast(F8, vr), pf[qb][kb][s2], oa[qb]);
+            }
+        lds_barrier();                                   // every wave has read this V chunk
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            const int qs = qb * 32 + r, qtx = qs & 7, qty = qs >> 3;
+            const float inv = 1.0f / lt[qb];
+            if (wok && qtx >= c0 && qtx < c1 && qty < ws && !(FA_WIN_ABL & 4)) {
+                const int px = ax + qtx - X0;
+#pragma unroll
+                for (int x = 0; x < 16; ++x)
+                    *(T*)(img + acc_row(x, h) * 1024 + qty * 128 + px * 2) = (T)(oa[qb][x] * inv);
+            }
+        }
+        lds_barrier();
+        constexpr int NU = 32 * 8 * 8;                   // (feature, row, 16-B chunk) units: a wave covers
+#pragma unroll                                           // 8 rows x 8 chunks of one feature
+        for (int it = 0; it < NU / 512; ++it) {
+            const int u = it * 512 + tid, f = u >> 6, row = (u >> 3) & 7, j = u & 7;
+            const int y = y0 + row, fg = vc * 32 + f, x0 = X0 + 8 * j;
+            if (row >= ws || y < 0 || y >= H_ || fg >= dv || x0 + 8 <= xlo || x0 >= xhi || (FA_WIN_ABL & 8)) continue;
+            const int go = ((fg * P_ + y * W_ + x0) * 2);
+            const char* src = img + f * 1024 + row * 128 + j * 16;
+            if (x0 >= xlo && x0 + 8 <= xhi) {
+                __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)src, ors, go, 0, 0);
+            } else if (!(FA_WIN_ABL & 16)) {             // a chunk shared with the neighbour strip
+                for (int e = 0; e < 8; ++e)
+                    if (x0 + e >= xlo && x0 + e < xhi)
+                        __builtin_amdgcn_raw_buffer_store_b16(*(const unsigned short*)(src + 2 * e), ors, go + 2 * e, 0, 0);
+            }
+        }
+        if (vc == 0) FA_STAMP(4);
+    }
+    FA_STAMP(5);
+}
+
+// --------------------------------------------------------------------------
 // Segment-owning windowed forward (bf16/f16, 2-D, stride >= ws, ws <= 7,
 // d, dv <= 64, width % 32 == 0, 16-B aligned q, k, v, y; mode 9, §2.3).
 //
@@ -1963,7 +2234,7 @@ static bool rows_f32_ok(const WindowedArgs& a) {
            a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
 }
 
-thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default)
+thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default for small launches), 10 eight-window strip (the default from kStripMin strips on)
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
@@ -2005,10 +2276,44 @@ static int rows_kind(const WindowedArgs& a) {
     return a.g.L * a.batch >= kRows4Min ? 4 : 1;
 }
 
+// Strip kernel (win_strip) from this many workgroups on: below it the eight-window
+// workgroups leave CUs idle and the two-window kernel's latency wins (configs[2] at
+// B = 1 is 57 strips).
+constexpr int64_t kStripMin = 512;
+
+// Windows of the first strip: the smallest k0 in 1..8 with k0 * ws = pad (mod 8),
+// so that every later strip starts on a 16-B chunk of y (8 otherwise).
+static int strip_first(const WindowGeom& g) {
+    for (int k0 = 1; k0 <= kStripW; ++k0)
+        if (((k0 * g.ws - g.pad) % 8 + 8) % 8 == 0) return k0;
+    return kStripW;
+}
+static int64_t strip_count(const WindowGeom& g, int k0) {
+    return g.O[0] <= k0 ? 1 : 1 + (g.O[0] - k0 + kStripW - 1) / kStripW;
+}
+
+// Whether the forward picks the strip kernel for this geometry (no pointers).
+static bool strip_applies(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
+    if ((dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16) || g.nsp != 2 || g.stride != g.ws || g.ws > 7 ||
+        g.S[0] % 8 != 0 || d > 64 || dv > 64 || (g_win_force_composed != 0 && g_win_force_composed != 10))
+        return false;
+    const int64_t nsx = strip_count(g, strip_first(g)), nstrip = nsx * g.O[1] * batch;
+    if (nstrip >= INT32_MAX || g.P * (d > dv ? d : dv) * 2 >= INT32_MAX || g.L * batch >= INT32_MAX) return false;
+    return g_win_force_composed == 10 || nstrip >= kStripMin;
+}
+
 template <class T, int D, int DV>
 static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
     if (a.g.ws <= 7 && g_win_force_composed != 5) {
         const int64_t nw = a.g.L * a.batch;
+        if (strip_applies(a.dtype, a.g, a.d, a.dv, a.batch) && ((uintptr_t)a.y & 15u) == 0) {
+            const int k0 = strip_first(a.g);
+            const int64_t nsx = strip_count(a.g, k0), nstrip = nsx * a.g.O[1] * a.batch;
+            hipLaunchKernelGGL((win_strip<T, D, DV>), dim3((unsigned)nstrip), dim3(512), 0, s, (const T*)a.q,
+                               (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, (int)nsx, k0,
+                               (int)nstrip, a.scale, a.scale * kLog2e);
+            return hipGetLastError();
+        }
         const bool two_img_ok = 2 * a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX;
         const bool seg_ok = a.g.S[0] % 32 == 0 && ((uintptr_t)a.y & 15u) == 0 &&
                             a.batch * a.g.O[1] * (a.g.S[0] / 32) < INT32_MAX;
@@ -2093,7 +2398,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
     const size_t tok = (size_t)(g.T * g.L * batch);
-    if (fused_ok(dtype, g, d, dv))   // direct (no overlap): nothing; overlap: the window outputs
+    if (fused_ok(dtype, g, d, dv))   // direct (no overlap): none; overlap: the window outputs
         return g.stride >= g.ws ? 0 : align256(tok * dv * esize(dtype)) + 256;
     return align256(tok * d * esize(dtype)) * 2 + align256(tok * dv * esize(dtype)) * 2 +
            align256(dense_fwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) + 256;

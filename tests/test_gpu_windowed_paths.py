@@ -2,7 +2,7 @@
 (fa_debug_set_win_composed: 1 composed gather→dense→fold, 2 register-gather,
 3 one-window row-shift (ws <= 7) / row-scatter (ws = 8), 4 four-window
 row-staged, 5 one-window row-scatter, 6 two-window row-shift, 7 / 8 two- / four-window LDS-DMA
-with rotated slots and analytic padding columns), against the oracle restatement of
+with rotated slots and analytic padding columns, 10 the eight-window strip kernel), against the oracle restatement of
 windowed_fa (src/windowed.jl:3-23, NNlib unfold/fold geometry) on geometries
 chosen for the row-staged kernels' edge handling: windows hanging over the
 left / right / bottom image edge, odd and even window x-starts (the row-shift
@@ -45,7 +45,7 @@ def _np(t):
     return t.detach().float().cpu().numpy().astype(np.float64)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10])
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
 def test_windowed_forced_path(fa, geom, path):
     W, H, ws, st, pad = geom
@@ -186,7 +186,7 @@ def test_windowed_backward_f32_paths(fa, geom, path):
         L.fa_debug_set_win_composed(old)
 
 
-@pytest.mark.parametrize("path", [0, 3, 6, 7, 8])
+@pytest.mark.parametrize("path", [0, 3, 6, 7, 8, 10])
 def test_windowed_nonfinite_stays_in_its_window(fa, path):
     """An inf in one pixel's k and v reaches only the window holding that pixel, as in
     the reference, where windows are disjoint token sets.  The fused kernels load 8-pixel
@@ -267,3 +267,70 @@ def test_windowed_segment_kernel(fa, geom):
         y6, l6, m6 = outs[6]
         assert torch.equal(y.view(torch.int16), y6.view(torch.int16)), f"y not bitwise equal to mode 6 ({tag})"
         assert torch.equal(l, l6) and torch.equal(m, m6), f"l, m not bitwise equal to mode 6 ({tag})"
+
+
+STRIP_GEOMS = [  # stride == ws, width % 8 == 0 (the strip kernel's eligibility)
+    (32, 20, 7, 7, 3),      # 6 windows: one partial strip
+    (128, 16, 7, 7, 3),     # configs[2]'s width: 19 windows = 8 + 8 + 3
+    (120, 9, 7, 7, 0),      # 17 windows, the last pixels uncovered (NaN)
+    (64, 13, 6, 6, 2),
+    (72, 12, 5, 5, 2),
+    (64, 17, 3, 3, 1),
+    (16, 8, 7, 7, 6),       # pad close to ws: windows hang over both edges
+    (112, 10, 7, 7, 5),
+    (64, 12, 4, 4, 1),      # even ws, odd pad: no first-strip width aligns the strip ends (2-B end stores)
+    (48, 10, 6, 6, 1),
+    (200, 9, 7, 7, 3),      # 29 windows: first strip 5 (ends on 16-B chunks), then 8 + 8 + 8
+]
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("geom", STRIP_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_strip_kernel(fa, geom, dtype):
+    """Mode 10 (win_strip: eight adjacent windows per workgroup, channel-streamed LDS-DMA,
+    y stored as 16-B chunks of the strip) vs the oracle, and bitwise vs the two-window
+    LDS-DMA kernel (mode 7), whose rotated-slot arithmetic it repeats window by window."""
+    W, H, ws, st, pad = geom
+    tdt = torch.bfloat16 if dtype == "bfloat16" else torch.float16
+    rng = np.random.default_rng(W * 37 + H * 11 + ws)
+    cast = lambda a: torch.tensor(a).to(tdt).double().numpy()
+    L = fa.lib()
+    for (d, dv) in DIMS:
+        B = 3
+        q, k = (cast(rng.standard_normal((W, H, d, B))) for _ in range(2))
+        v = cast(rng.standard_normal((W, H, dv, B)))
+        outs = {}
+        for path in (10, 7):
+            old = L.fa_debug_set_win_composed(path)
+            try:
+                outs[path] = fa.windowed_fa(*(fa.jl_tensor(a, tdt) for a in (q, k, v)), ws, stride=st, pad=pad)
+                torch.cuda.synchronize()
+            finally:
+                L.fa_debug_set_win_composed(old)
+        y, l, m = outs[10]
+        yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
+        tag = f"d {d} dv {dv}"
+        assert_close(_np(y), yr, dtype, f"y ({tag})", nan_ok=True)
+        assert_lm_close(_np(l), lr, dtype, f"l ({tag})")
+        assert_lm_close(_np(m), mr, dtype, f"m ({tag})")
+        y7, l7, m7 = outs[7]
+        assert torch.equal(y.view(torch.int16), y7.view(torch.int16)), f"y not bitwise equal to mode 7 ({tag})"
+        assert torch.equal(l, l7) and torch.equal(m, m7), f"l, m not bitwise equal to mode 7 ({tag})"
+
+
+def test_windowed_strip_full_size(fa):
+    """configs[2] at B = 32 runs the strip kernel by default (>= kStripMin strips): the
+    oracle on two images, and the rows / pixels no other path wrote are all set."""
+    W = H = 128
+    B, d = 32, 64
+    g = torch.Generator(device="cuda").manual_seed(9)
+    q, k, v = (fa.jl_tensor(torch.randn((W, H, d, B), generator=g, device="cuda"), torch.bfloat16) for _ in range(3))
+    y, l, m = fa.windowed_fa(q, k, v, 7)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all()
+    for b in (0, 31):
+        sl = lambda t: _np(t[..., b:b + 1])
+        yr, lr, mr = O.windowed_fa(sl(q), sl(k), sl(v), 7, 7, 3)
+        assert_close(sl(y), yr, "bfloat16", f"y image {b}")
+        assert_lm_close(_np(l[:, :, :, b:b + 1]), lr, "bfloat16", f"l image {b}")
+        assert_lm_close(_np(m[:, :, :, b:b + 1]), mr, "bfloat16", f"m image {b}")

@@ -10,7 +10,9 @@ import fa_hip
 from bench import time_graph
 L = fa_hip.lib()
 L.fa_debug_set_win_composed.argtypes = [ctypes.c_int]
-NAMES = {0: "auto    ", 3: "rows1   ", 6: "rows1x2 ", 4: "rows4   ", 2: "gather  ", 1: "composed"}
+NAMES = {0: "auto    ", 3: "rows1   ", 6: "rows1x2 ", 4: "rows4   ", 2: "gather  ", 1: "composed", 7: "dma2    ",
+         10: "strip8  "}
+MODES = [int(x) for x in os.environ.get("WMODES", "0,3,6,4,2").split(",")]
 Bs = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8, 32, 128]
 for B in Bs:
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -18,14 +20,15 @@ for B in Bs:
     T, Lw = 49, 361
     alg = B * (4 * 128 * 128 * 64 * 2 + 2 * T * Lw * 4)
     res = {}
-    for comp in (0, 3, 6, 4, 2):
+    for comp in MODES:
         L.fa_debug_set_win_composed(comp)
         y, l, m = fa_hip.windowed_fa(q, k, v, 7)
         torch.cuda.synchronize()
         res[comp] = (y.float(), l.clone())
         t = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), 20)
         print(f"B={B:4d} {NAMES[comp]}: {t*1e6:9.1f} us  {alg/t/1e9:8.1f} GB/s", flush=True)
-    for c in (0, 3, 6, 2):
-        dy = (res[c][0] - res[4][0]).abs().max()
-        print(f"   {c} vs rows4: max|dy| {float(dy):.3e}  max|dl| {float((res[c][1]-res[4][1]).abs().max()):.3e}")
+    ref = MODES[-1]
+    for c in MODES[:-1]:
+        dy = (res[c][0] - res[ref][0]).abs().max()
+        print(f"   {c} vs {ref}: max|dy| {float(dy):.3e}  max|dl| {float((res[c][1]-res[ref][1]).abs().max()):.3e}")
     L.fa_debug_set_win_composed(0)
