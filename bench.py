@@ -325,8 +325,11 @@ def cfg2_block(fa, dist, steps=20):
     pad 3: 19x19 windows of 49 tokens), d 64 (reference src/windowed.jl:3-23,
     src/utils.jl:36-54); forward and backward at B = 1 (as written) and
     B = 32.  HBM-bound (26 FLOP/B): algorithmic bytes = q, k, v read + y
-    written (+ l, m) for the forward; q, k, v, y, dy read + dq, dk, dv written
-    (+ l, m) for the backward; GB/s against 8 TB/s."""
+    written (+ l, m) for the forward; q, k, v, dy read + dq, dk, dv written
+    (+ l, m) for the backward (y is not needed: the strip backward forms
+    D = rowsum(P ∘ dP); the one-window kernel still reads it); GB/s against 8 TB/s.
+    Kernels: B = 1 runs the per-window kernels, B = 32 the strip kernels
+    (>= 512 / 256 strips)."""
     gen = torch.Generator(device="cuda").manual_seed(11)
     T, L, S, dd = 49, 19 * 19, 128 * 128, 64
     res = {"workload": "configs[2]: windowed_fa 2-D bf16, 128x128 image, ws=7, d=64, stride 7, pad 3",
@@ -337,12 +340,14 @@ def cfg2_block(fa, dist, steps=20):
         by = Bimg * (4 * S * dd * 2 + 2 * T * L * 4)
         y, lw, mw = fa.windowed_fa(q, k, v, 7)
         tb = time_graph(lambda: fa.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), max(5, steps // 2), dist)
-        bb = Bimg * (8 * S * dd * 2 + 2 * T * L * 4)
+        bb = Bimg * (7 * S * dd * 2 + 2 * T * L * 4)
         res[f"B{Bimg}"] = {
             "fwd_us": t * 1e6, "fwd_GBs": by / t / 1e9, "fwd_frac_hbm": by / t / 1e9 / PEAK_HBM_GBS,
-            "fwd_bytes": by, "fwd_kernel": "fa::win_rows1s<bf16,64,64,2>",
+            "fwd_bytes": by,
+            "fwd_kernel": "fa::win_strip<bf16,64,64>" if Bimg >= 9 else "fa::win_rows1s<bf16,64,64,2>",
             "bwd_us": tb * 1e6, "bwd_GBs": bb / tb / 1e9, "bwd_frac_hbm": bb / tb / 1e9 / PEAK_HBM_GBS,
-            "bwd_bytes": bb, "bwd_kernel": "fa::win_bwd_rows<bf16,64,64>"}
+            "bwd_bytes": bb,
+            "bwd_kernel": "fa::win_bwd_strip<bf16,64,64>" if Bimg >= 5 else "fa::win_bwd_rows<bf16,64,64>"}
         del q, k, v, dy, y, lw, mw
     torch.cuda.empty_cache()
     return res

@@ -32,7 +32,8 @@
 // Timing-only ablations of win_rows1s (tools/exp/win_ablate.hip; 0 in the product):
 // 1 = no y stores, 2 = every row load from one address; of win_strip
 // (tools/exp/strip_stamp.py): 4 = no y strip-image writes, 8 = no y global stores,
-// 16 = no 2-B stores of the chunks shared with a neighbour strip
+// 16 = no 2-B stores of the chunks shared with a neighbour strip; of win_bwd_strip
+// (tools/exp/bwd_strip_stamp.py): 32 = no gradient stores
 #ifndef FA_WIN_ABL
 #define FA_WIN_ABL 0
 #endif
@@ -731,6 +732,41 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
+// LDS accesses hidden from the compiler (inline asm).  hipcc makes every LDS access
+// it can see wait for ALL outstanding LDS-DMA (s_waitcnt vmcnt(0)): it cannot tell
+// the DMA's destination buffer from the one being read, so a multi-buffer DMA
+// pipeline would drain at every step.  An asm read's result is NOT ready until
+// lds_wait(); pass it through lds_fence() after that wait, before any use.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ s16x4 lds_tr16(const void* p) {
+    s16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_off(p)) : "memory");
+    return r;
+}
+__device__ __forceinline__ u32x4 lds_b128(const void* p) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(lds_off(p)) : "memory");
+    return r;
+}
+__device__ __forceinline__ u32x2 lds_b64(const void* p) {
+    u32x2 r;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(lds_off(p)) : "memory");
+    return r;
+}
+__device__ __forceinline__ float lds_b32(const void* p) {
+    float r;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(lds_off(p)) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_w16(void* p, unsigned v) {
+    asm volatile("ds_write_b16 %0, %1" : : "v"(lds_off(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <class X>
+__device__ __forceinline__ void lds_fence(X& x) { asm volatile("" : "+v"(x)); }
+
 // Per-lane variant of shift_row (windows of one workgroup differ in shift).
 __device__ __forceinline__ u32x4 shift_row_lane(const u32x4& in, int sh, const unsigned (&mask)[4]) {
     const int s2 = sh >> 1;
@@ -1230,7 +1266,10 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
     constexpr int NQC = D / 16, NVC = DV / 32;       // Q/K chunks of 16 features, V chunks of 32
     constexpr int NLD = NQC + NVC;                   // image loads, alternating between the two buffers
     constexpr int BUF = 32768;
-    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];   // 64 KB: two workgroups per CU
+    // two separate LDS objects (not one array): the compiler's LDS-DMA wait tracking tells
+    // them apart, so a read of one buffer does not wait for the DMA into the other
+    __shared__ __attribute__((aligned(16))) char sbuf0[BUF], sbuf1[BUF];   // 64 KB: two workgroups per CU
+    auto bufp = [&](int i) __attribute__((always_inline)) { return (i & 1) ? sbuf1 : sbuf0; };
 
     FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -1266,7 +1305,7 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
     // image load i (QK chunk i, then V chunk i - NQC) into buffer i & 1: 32 DMA
     // instructions (one feature row each), 4 per wave
     auto issue = [&](__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, int i) {
-        char* buf = smem + (i & 1) * BUF;
+        char* buf = bufp(i);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int rr = j * 8 + wave;                  // 0..31
@@ -1307,17 +1346,29 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         lds_barrier();
         if (cc == 0) FA_STAMP(1);
-        const char* buf = smem + (cc & 1) * BUF;
+        const char* buf = bufp(cc);
         // tr-read rows 8h + qq (+4): chunk-local features; slot rows 4blk + 2kh + (sig >> 1) / qb*4 + 2kh + (pp >> 1)
-        F8 kf[2], qf[2];
+        // (asm reads: the next buffer's DMA stays in flight)
+        s16x4 rk[2][2], rq[2][2];
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
             const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
-            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
-                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 1024)), 0, 1, 2, 3, 4, 5, 6, 7);
+            rk[blk][0] = lds_tr16(a);
+            rk[blk][1] = lds_tr16(a + 4 * 1024);
             const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
-            qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(aq)),
-                                              __builtin_bit_cast(F4, ds_read_tr16(aq + 4 * 1024)), 0, 1, 2, 3, 4, 5, 6, 7);
+            rq[blk][0] = lds_tr16(aq);
+            rq[blk][1] = lds_tr16(aq + 4 * 1024);
+        }
+        lds_wait();
+        F8 kf[2], qf[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { lds_fence(rk[blk][i]); lds_fence(rq[blk][i]); }
+            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rk[blk][0]), __builtin_bit_cast(F4, rk[blk][1]),
+                                              0, 1, 2, 3, 4, 5, 6, 7);
+            qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rq[blk][0]), __builtin_bit_cast(F4, rq[blk][1]),
+                                              0, 1, 2, 3, 4, 5, 6, 7);
         }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -1396,7 +1447,7 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
         vm[j] = ((2 * j >= c0 && 2 * j < c1) ? 0x0000FFFFu : 0u) | ((2 * j + 1 >= c0 && 2 * j + 1 < c1) ? 0xFFFF0000u : 0u);
 #pragma unroll
     for (int vc = 0; vc < NVC; ++vc) {
-        char* img = smem + ((NQC + vc) & 1) * BUF;
+        char* img = bufp(NQC + vc);
         f32x16 oa[2];
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
@@ -1911,6 +1962,404 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         }
     }
     FA_STAMP(4);
+    FA_STAMP(5);
+}
+
+// --------------------------------------------------------------------------
+// Strip BACKWARD: the eight windows of a forward strip per workgroup, one per
+// wave (bf16/f16, 2-D, stride == ws <= 7, d, dv <= 64, width % 8 == 0, 16-B
+// aligned tensors; the default from kStripBwdMin strips on).  Same strip
+// geometry, rotated slots and swizzled LDS-DMA images as win_strip; every
+// gradient leaves as whole 16-B chunks of the strip's pixels.
+//
+//   phase A  (16-feature chunks, Sᵀ-style images): dPᵀ = V·dOᵀ, then Sᵀ = K·Qᵀ,
+//            keys on accumulator rows, queries on lanes, as in the forward;
+//            P = exp(τS − lse) from the forward's (l, m), read by a dword DMA;
+//            D = rowsum(P ∘ dP) in-lane (= rowsum(dO ∘ y): y is never read);
+//            dS = P ∘ (dP − D).  P and dS become bf16 B fragments (n = query).
+//   phase B  (32-feature chunks, row images), one output chunk per load:
+//            dQᵀ = τ Kᵀ dSᵀ straight from the fragments; Pᵀ and dSᵀ with keys
+//            on lanes by an identity MFMA (C = A·I with the fragments as A:
+//            exact, no LDS round trip); dKᵀ = τ Qᵀ dS, dVᵀ = dOᵀ P.  Each output
+//            chunk is written as a strip image [32 f][8 rows][64 px] over the
+//            chunk just read and stored as 16-B chunks.
+//   loads    : a ring of four 32-KB buffers, three loads in flight behind the
+//            one being read (counted vmcnt over the DMAs; the gradient stores
+//            in between only make a wait stronger), LDS-only barriers.
+// Keys / queries outside the window (slot row >= ws, columns outside [c0, c1),
+// rows outside the image) are masked to P = dS = 0 by selects, so a non-finite
+// neighbour pixel never enters this window's sums.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void wait_vm(int n) {   // n: a constant once the step loops are unrolled
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
+}
+
+// The strip image [32 f][8 rows][64 px] (pixel X0 + px) of output features
+// fbase .. fbase + 31 as 16-B chunk stores; chunks that straddle the strip ends
+// (only when no first-strip width aligns them) as 2-B stores.
+template <class T>
+__device__ __forceinline__ void strip_store(const char* img, __amdgpu_buffer_rsrc_t ors, int tid, int fbase, int C,
+                                            int y0, int ws, int H_, int W_, int P_, int X0, int xlo, int xhi) {
+    if (FA_WIN_ABL & 32) return;
+    u32x4 val[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) val[it] = lds_b128(img + (it * 512 + tid) * 16);   // unit u at byte 16 u
+    lds_wait();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) lds_fence(val[it]);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int u = it * 512 + tid, f = u >> 6, row = (u >> 3) & 7, j = u & 7;
+        const int y = y0 + row, fg = fbase + f, x0 = X0 + 8 * j;
+        if (row >= ws || y < 0 || y >= H_ || fg >= C || x0 + 8 <= xlo || x0 >= xhi) continue;
+        const int go = (fg * P_ + y * W_ + x0) * 2;
+        if (x0 >= xlo && x0 + 8 <= xhi) {
+            __builtin_amdgcn_raw_buffer_store_b128(val[it], ors, go, 0, 0);
+        } else {
+            for (int e = 0; e < 8; ++e)
+                if (x0 + e >= xlo && x0 + e < xhi)
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(val[it][e >> 1] >> (16 * (e & 1))), ors,
+                                                          go + 2 * e, 0, 0);
+        }
+    }
+}
+
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q, const T* __restrict__ k,
+                                                        const T* __restrict__ v, const T* __restrict__ dy,
+                                                        const float* __restrict__ lw, const float* __restrict__ mw,
+                                                        T* __restrict__ dq, T* __restrict__ dk, T* __restrict__ dvo,
+                                                        WinDev g, int d, int dv, int nsx, int k0, int nwg,
+                                                        float scale, float scale_log2) {
+    typedef typename Frag8<T>::type F8;
+    typedef typename Frag8<T>::half F4;
+    static_assert(D % 32 == 0 && D <= 64 && DV % 32 == 0 && DV <= 64, "head dims");
+    constexpr int NOV = DV / 16, NA = NOV + D / 16;   // phase A loads: (dO, V), then (Q, K) 16-feature chunks
+    constexpr int NBK = D / 32, NBQ = D / 32, NBO = DV / 32;
+    constexpr int NL = NA + NBK + NBQ + NBO;          // phase B loads: K (dQ), Q (dK), dO (dV) 32-feature chunks
+    constexpr int R = 4, BUF = 32768;
+    __shared__ __attribute__((aligned(16))) char smem[R * BUF + 2 * 8 * 64 * 4];
+    float* const ls = (float*)(smem + R * BUF);       // l, m of the strip's windows: [window][64]
+    float* const ms = ls + 8 * 64;
+
+    FA_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride, nwx = g.O[0];
+    const int lid = xcd_remap(blockIdx.x, nwg);
+    const int sxi = lid % nsx, t0 = lid / nsx, wy = t0 % g.O[1], b = t0 / g.O[1];
+    const int wx0 = sxi == 0 ? 0 : k0 + (sxi - 1) * kStripW, y0 = wy * st - g.pad;
+    const int nvalid = min(sxi == 0 ? k0 : kStripW, nwx - wx0);
+    auto ax_of = [&](int w) __attribute__((always_inline)) { return min(max(((wx0 + w) * st - g.pad) & ~1, 0), W_ - 8); };
+    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    const auto ors = slab_rsrc(dy + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    const int64_t wrow = (int64_t)g.T * ((int64_t)nwx * wy + (int64_t)g.L * b);   // l, m of window (0, wy)
+    const auto lrs = slab_rsrc(lw + wrow, (uint32_t)(g.T * nwx * 4));
+    const auto mrs = slab_rsrc(mw + wrow, (uint32_t)(g.T * nwx * 4));
+
+    // one DMA instruction = one feature row fl of an image: lane -> (slot row, window)
+    auto dma_qk = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg, int C) __attribute__((always_inline)) {   // Sᵀ-style image (tr reads)
+        const int pc = lane >> 3, pw = lane & 7;
+        const int w = pw ^ ((fl & 3) | (((pc >> 1) & 1) << 2)), y = y0 + pc;
+        const bool ok = w < nvalid && pc < ws && y >= 0 && y < H_ && fg < C;
+        const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
+                                                 off, 0, 0, 0);
+    };
+    auto dma_row = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg, int C) __attribute__((always_inline)) {  // row image (16-B / 8-B reads)
+        const int c = (lane >> 3) ^ ((fl >> 3) & 1), w = (lane & 7) ^ (fl & 7), y = y0 + c;
+        const bool ok = w < nvalid && c < ws && y >= 0 && y < H_ && fg < C;
+        const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
+                                                 off, 0, 0, 0);
+    };
+    // load j into buffer j % R: 32 DMA instructions (one feature row each), 4 per wave
+    auto issue = [&](__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr,
+                     __amdgpu_buffer_rsrc_t orr, int j) __attribute__((always_inline)) {
+        char* buf = smem + (j % R) * BUF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rr = i * 8 + wave;                 // 0..31
+            if (j < NOV) {
+                if (rr < 16) dma_qk(orr, buf, rr, j * 16 + rr, dv);
+                else dma_qk(vr, buf + 16384, rr - 16, j * 16 + rr - 16, dv);
+            } else if (j < NA) {
+                if (rr < 16) dma_qk(qr, buf, rr, (j - NOV) * 16 + rr, d);
+                else dma_qk(kr, buf + 16384, rr - 16, (j - NOV) * 16 + rr - 16, d);
+            } else if (j < NA + NBK) {
+                dma_row(kr, buf, rr, (j - NA) * 32 + rr, d);
+            } else if (j < NA + NBK + NBQ) {
+                dma_row(qr, buf, rr, (j - NA - NBK) * 32 + rr, d);
+            } else {
+                dma_row(orr, buf, rr, (j - NA - NBK - NBQ) * 32 + rr, dv);
+            }
+        }
+    };
+    {   // l, m of this wave's window (64 dwords per window, lanes >= T read 0), ahead of load 0
+        const int w = wave;
+        const int off = (w < nvalid && lane < g.T) ? (g.T * (wx0 + w) + lane) * 4 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (__attribute__((address_space(3))) void*)(ls + w * 64), 4, off,
+                                                 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(mrs, (__attribute__((address_space(3))) void*)(ms + w * 64), 4, off,
+                                                 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) issue(qrs, krs, vrs, ors, j);
+
+    // ---- this wave's window ----
+    const int wl = wave;
+    const bool wok = wl < nvalid;
+    const int wx = wx0 + wl, xs = wx * st - g.pad, ax = ax_of(wl);
+    const int c0 = xs - ax, c1 = c0 + ws;
+    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+    auto slot_ok = [&](int s) __attribute__((always_inline)) {                          // slot s of this window: a real token of the image
+        const int sx = s & 7, sy = s >> 3;
+        return wok && sy < ws && sx >= c0 && sx < c1 && y0 + sy >= 0 && y0 + sy < H_;
+    };
+    // step j: wait for load j (the loads issued after it stay in flight), LDS barrier
+    auto step_wait = [&](int j) __attribute__((always_inline)) {
+        wait_vm(4 * min(R - 1, NL - 1 - j));
+        lds_barrier();
+    };
+
+    f32x16 sa[2][2], pa[2][2];                           // Sᵀ, dPᵀ: [key block][query block]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) sa[kb][qb][x] = pa[kb][qb][x] = 0.0f;
+
+    // ---- phase A ----
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        step_wait(j);
+        if (j == 0) FA_STAMP(1);
+        const char* buf = smem + (j % R) * BUF;
+        s16x4 rk[2][2], rq[2][2];                        // keys (V / K, permuted), queries (dO / Q)
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+            const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
+            rk[blk][0] = lds_tr16(a);
+            rk[blk][1] = lds_tr16(a + 4 * 1024);
+            const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
+            rq[blk][0] = lds_tr16(aq);
+            rq[blk][1] = lds_tr16(aq + 4 * 1024);
+        }
+        lds_wait();
+        F8 kf[2], qf[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { lds_fence(rk[blk][i]); lds_fence(rq[blk][i]); }
+            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rk[blk][0]), __builtin_bit_cast(F4, rk[blk][1]),
+                                              0, 1, 2, 3, 4, 5, 6, 7);
+            qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rq[blk][0]), __builtin_bit_cast(F4, rq[blk][1]),
+                                              0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                if (j < NOV) pa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], pa[kb][qb]);
+                else sa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], sa[kb][qb]);
+            }
+        if (j + R < NL) {
+            lds_barrier();                               // every wave is done with this buffer
+            issue(qrs, krs, vrs, ors, j + R);
+        }
+    }
+    FA_STAMP(2);
+
+    // ---- P, D, dS per query (lane) ----
+    F8 pf[2][2][2], dsf[2][2][2];                        // [query block][key block][16-key half]
+    float lq[2], mq[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        const int qs = qb * 32 + r;
+        const int tq = slot_ok(qs) ? (qs >> 3) * ws + (qs & 7) - c0 : 0;   // window token of the query slot
+        lq[qb] = lds_b32(ls + wl * 64 + tq);
+        mq[qb] = lds_b32(ms + wl * 64 + tq);
+    }
+    lds_wait();
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        lds_fence(lq[qb]);
+        lds_fence(mq[qb]);
+        const int qs = qb * 32 + r;
+        const bool qv = slot_ok(qs);
+        const float nl = qv ? (mq[qb] + __logf(lq[qb])) * kLog2e : 0.0f;
+        float dsum = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
+                const bool ok = qv && slot_ok(kt);
+                const float pr = ok ? exp2_fast(fmaf(sa[kb][qb][x], scale_log2, -nl)) : 0.0f;
+                sa[kb][qb][x] = pr;
+                pa[kb][qb][x] = ok ? pa[kb][qb][x] : 0.0f;
+                dsum = fmaf(pr, pa[kb][qb][x], dsum);
+            }
+        const float Dq = swap_halves_sum(dsum);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                pf[qb][kb][x >> 3][x & 7] = (T)sa[kb][qb][x];
+                dsf[qb][kb][x >> 3][x & 7] = (T)(sa[kb][qb][x] * (pa[kb][qb][x] - Dq));
+            }
+    }
+    FA_STAMP(3);
+
+    // ---- phase B ----
+    const int xs0 = wx0 * st - g.pad, X0 = xs0 & ~7;     // strip start, its 16-B aligned base
+    const int xlo = max(xs0, 0), xhi = min(xs0 + nvalid * ws, W_);
+    const auto dqs = slab_rsrc(dq + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto dks = slab_rsrc(dk + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
+    const auto dvs = slab_rsrc(dvo + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    unsigned cm[4];                                      // slot-column mask of a 16-B row fragment
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        cm[j] = ((2 * j >= c0 && 2 * j < c1) ? 0x0000FFFFu : 0u) | ((2 * j + 1 >= c0 && 2 * j + 1 < c1) ? 0xFFFF0000u : 0u);
+    // write a 32 x 32 block (features on accumulator rows, slot s on the lane) into the strip image
+    auto img_write = [&](char* img, const f32x16& acc, float mul, int s) __attribute__((always_inline)) {
+        if (slot_ok(s)) {
+            const int px = ax + (s & 7) - X0, row = s >> 3;
+#pragma unroll
+            for (int x = 0; x < 16; ++x)
+                lds_w16(img + acc_row(x, h) * 1024 + row * 128 + px * 2,
+                        __builtin_bit_cast(unsigned short, (T)(acc[x] * mul)));
+        }
+    };
+    // 16 query slots 16 s' + 4h + {0..3, 8..11} of block qb, feature r of a row image (the
+    // B-fragment order of an identity-transposed block), column-masked
+    // (asm reads: lds_wait + lds_fence before use)
+    auto frag_perm = [&](const char* buf, int qb, int s_, u32x2& lo, u32x2& hi) __attribute__((always_inline)) {
+        lo = lds_b64(buf + sv_pos(r, qb * 4 + 2 * s_, wl) + 8 * h);
+        hi = lds_b64(buf + sv_pos(r, qb * 4 + 2 * s_ + 1, wl) + 8 * h);
+    };
+    // one-hot B fragment: element e of lane (r, h) is 1 iff 16 s2 + 8 h + e == r
+    auto ident = [&](int s2) __attribute__((always_inline)) {
+        const int e = r - 16 * s2 - 8 * h;
+        const unsigned one = std::is_same<T, bf16>::value ? 0x3F80u : 0x3C00u;
+        u32x4 u = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (e == 2 * i) u[i] = one;
+            if (e == 2 * i + 1) u[i] = one << 16;
+        }
+        return __builtin_bit_cast(F8, u);
+    };
+    const F8 id0 = ident(0), id1 = ident(1);
+    // transpose: block (kb, qb) of X (B fragments, queries on lanes) -> keys on lanes, then
+    // B fragments [key block][query block][s'] in frag_perm's query order
+    auto transpose = [&](const F8 (&xf)[2][2][2], F8 (&xt)[2][2][2]) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                f32x16 c;
+#pragma unroll
+                for (int x = 0; x < 16; ++x) c[x] = 0.0f;
+                c = mfma32x32x16(xf[qb][kb][0], id0, c);
+                c = mfma32x32x16(xf[qb][kb][1], id1, c);
+#pragma unroll
+                for (int x = 0; x < 16; ++x) xt[kb][qb][x >> 3][x & 7] = (T)c[x];
+            }
+    };
+    auto step_end = [&](int j) __attribute__((always_inline)) {
+        if (j + R < NL) {
+            lds_barrier();                               // every wave has read the image
+            issue(qrs, krs, vrs, ors, j + R);
+        }
+    };
+
+    // dQᵀ = τ Kᵀ dSᵀ
+#pragma unroll
+    for (int c = 0; c < NBK; ++c) {
+        const int j = NA + c;
+        step_wait(j);
+        char* buf = smem + (j % R) * BUF;
+        f32x16 oa[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oa[qb][x] = 0.0f;
+        u32x4 kr[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) kr[kb][s2] = lds_b128(buf + sv_pos(r, kb * 4 + s2 * 2 + h, wl));
+        lds_wait();
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                lds_fence(kr[kb][s2]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) kr[kb][s2][i] &= cm[i];
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+                    oa[qb] = mfma32x32x16(__builtin_bit_cast(F8, kr[kb][s2]), dsf[qb][kb][s2], oa[qb]);
+            }
+        lds_barrier();                                   // every wave has read this K chunk
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) img_write(buf, oa[qb], scale, qb * 32 + r);
+        lds_barrier();
+        strip_store<T>(buf, dqs, tid, c * 32, d, y0, ws, H_, W_, P_, X0, xlo, xhi);
+        step_end(j);
+    }
+    FA_STAMP(4);
+
+    // dKᵀ = τ Qᵀ dS, dVᵀ = dOᵀ P (keys on lanes)
+#pragma unroll
+    for (int c = 0; c < NBQ + NBO; ++c) {
+        const int j = NA + NBK + c;
+        const bool isk = c < NBQ;
+        F8 xt[2][2][2];
+        transpose(isk ? dsf : pf, xt);
+        step_wait(j);
+        char* buf = smem + (j % R) * BUF;
+        f32x16 oa[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int x = 0; x < 16; ++x) oa[kb][x] = 0.0f;
+        u32x2 lo[2][2], hi[2][2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int s_ = 0; s_ < 2; ++s_) frag_perm(buf, qb, s_, lo[qb][s_], hi[qb][s_]);
+        lds_wait();
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int s_ = 0; s_ < 2; ++s_) {
+                lds_fence(lo[qb][s_]);
+                lds_fence(hi[qb][s_]);
+                const u32x4 u = {lo[qb][s_][0] & cm[2 * h], lo[qb][s_][1] & cm[2 * h + 1], hi[qb][s_][0] & cm[2 * h],
+                                 hi[qb][s_][1] & cm[2 * h + 1]};
+                const F8 a = __builtin_bit_cast(F8, u);
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) oa[kb] = mfma32x32x16(a, xt[kb][qb][s_], oa[kb]);
+            }
+        lds_barrier();
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) img_write(buf, oa[kb], isk ? scale : 1.0f, kb * 32 + r);
+        lds_barrier();
+        if (isk) strip_store<T>(buf, dks, tid, c * 32, d, y0, ws, H_, W_, P_, X0, xlo, xhi);
+        else strip_store<T>(buf, dvs, tid, (c - NBQ) * 32, dv, y0, ws, H_, W_, P_, X0, xlo, xhi);
+        step_end(j);
+    }
     FA_STAMP(5);
 }
 
@@ -2642,6 +3091,20 @@ static bool bwd_rows_ok(const WindowedBwdArgs& a) {
            a.g.P * 128 * 2 < INT32_MAX;
 }
 
+// The strip backward (win_bwd_strip): the forward strip kernel's shapes, d, dv <= 64,
+// 16-B aligned gradients too; from kStripBwdMin strips on (or forced by mode 10).
+constexpr int64_t kStripBwdMin = 256;
+static bool bwd_strip_ok(const WindowedBwdArgs& a) {
+    auto al = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+    if ((a.dtype != FA_DTYPE_BF16 && a.dtype != FA_DTYPE_F16) || a.g.nsp != 2 || a.g.stride != a.g.ws || a.g.ws > 7 ||
+        a.g.S[0] % 8 != 0 || a.d > 64 || a.dv > 64 || !al(a.q) || !al(a.k) || !al(a.v) || !al(a.dy) || !al(a.dq) ||
+        !al(a.dk) || !al(a.dv_) || (g_win_force_composed != 0 && g_win_force_composed != 10))
+        return false;
+    const int64_t nstrip = strip_count(a.g, strip_first(a.g)) * a.g.O[1] * a.batch;
+    if (nstrip >= INT32_MAX || a.g.P * 64 * 2 >= INT32_MAX || a.g.T * a.g.O[0] * 4 >= INT32_MAX) return false;
+    return g_win_force_composed == 10 || nstrip >= kStripBwdMin;
+}
+
 template <class T>
 static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
     const WinDev g = to_dev(a.g);
@@ -2653,6 +3116,25 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
             *why = hipGetErrorString(e);
             return FA_ERR_HIP;
         }
+    }
+    if (bwd_strip_ok(a)) {
+        const int k0 = strip_first(a.g);
+        const int64_t nsx = strip_count(a.g, k0), nstrip = nsx * a.g.O[1] * a.batch;
+#define FA_BWD_STRIP(DD, DVV)                                                                                   \
+    hipLaunchKernelGGL((win_bwd_strip<T, DD, DVV>), dim3((unsigned)nstrip), dim3(512), 0, s, (const T*)a.q,    \
+                       (const T*)a.k, (const T*)a.v, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk, (T*)a.dv_, g, \
+                       (int)a.d, (int)a.dv, (int)nsx, k0, (int)nstrip, a.scale, a.scale * kLog2e)
+        const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
+        if (Dc == 32 && DVc == 32) FA_BWD_STRIP(32, 32);
+        else if (Dc == 32) FA_BWD_STRIP(32, 64);
+        else if (DVc == 32) FA_BWD_STRIP(64, 32);
+        else FA_BWD_STRIP(64, 64);
+#undef FA_BWD_STRIP
+        if ((e = hipGetLastError()) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
+        return FA_OK;
     }
     const dim3 grid((unsigned)(a.g.L * a.batch));
 #define FA_BWD_ROWS(DD, DVV)                                                                                 hipLaunchKernelGGL((win_bwd_rows<T, DD, DVV>), grid, dim3(256), 0, s, (const T*)a.q, (const T*)a.k,                         (const T*)a.v, (const T*)a.y, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk,                              (T*)a.dv_, g, (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e)

@@ -334,3 +334,82 @@ def test_windowed_strip_full_size(fa):
         assert_close(sl(y), yr, "bfloat16", f"y image {b}")
         assert_lm_close(_np(l[:, :, :, b:b + 1]), lr, "bfloat16", f"l image {b}")
         assert_lm_close(_np(m[:, :, :, b:b + 1]), mr, "bfloat16", f"m image {b}")
+
+
+def _bwd_grads(fa, q, k, v, dy, ws, st, pad, dt, path):
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(path)
+    try:
+        Q, K, V, DY = (fa.jl_tensor(a, dt) for a in (q, k, v, dy))
+        y, l, m = fa.windowed_fa(Q, K, V, ws, stride=st, pad=pad)
+        g = fa.windowed_fa_backward(Q, K, V, y, DY, l, m, ws, stride=st, pad=pad)
+        torch.cuda.synchronize()
+        return g
+    finally:
+        L.fa_debug_set_win_composed(old)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("geom", STRIP_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
+def test_windowed_backward_strip_kernel(fa, geom, dtype):
+    """Mode 10 backward (win_bwd_strip: eight windows per workgroup, D = rowsum(P ∘ dP),
+    identity-MFMA transposes, 16-B gradient chunk stores) vs the oracle chain rule, and
+    close to the one-window kernel (mode 3, win_bwd_rows, D from y)."""
+    W, H, ws, st, pad = geom
+    tdt = torch.bfloat16 if dtype == "bfloat16" else torch.float16
+    rng = np.random.default_rng(W * 41 + H * 5 + ws)
+    cast = lambda a: torch.tensor(a).to(tdt).double().numpy()
+    for (d, dv) in DIMS:
+        B = 3
+        q, k = (cast(rng.standard_normal((W, H, d, B))) for _ in range(2))
+        v, dy = (cast(rng.standard_normal((W, H, dv, B))) for _ in range(2))
+        g10 = _bwd_grads(fa, q, k, v, dy, ws, st, pad, tdt, 10)
+        g3 = _bwd_grads(fa, q, k, v, dy, ws, st, pad, tdt, 3)
+        ref = O.windowed_fa_backward(q, k, v, dy, ws, st, pad)
+        for a, a3, b_, nm in zip(g10, g3, ref, ("dq", "dk", "dv")):
+            x, x3 = _np(a), _np(a3)
+            scale = max(np.abs(b_).max(), 1e-2)
+            err = np.abs(x - b_).max() / scale
+            assert np.all(np.isfinite(x)) and err <= 2e-2, f"d {d} dv {dv} {nm}: {err:.2e} vs the oracle"
+            err3 = np.abs(x - x3).max() / scale
+            assert err3 <= 2e-2, f"d {d} dv {dv} {nm}: {err3:.2e} vs mode 3"
+
+
+@pytest.mark.parametrize("path", [3, 10])
+def test_windowed_backward_nonfinite_stays_in_its_window(fa, path):
+    """An inf in one pixel's q, k, v and dy changes the gradients of that pixel's window
+    only: every other pixel's dq, dk, dv is bitwise the inf-free result (the neighbour
+    window's 8-pixel row loads hold the pixel, masked by selects)."""
+    W, H, ws, st, pad = 32, 20, 7, 7, 3
+    rng = np.random.default_rng(6)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    d = dv = 64
+    q, k, v, dy = (bf(rng.standard_normal((W, H, d, 1))) for _ in range(4))
+    clean = _bwd_grads(fa, q, k, v, dy, ws, st, pad, torch.bfloat16, path)
+    for a in (q, k, v, dy):
+        a[10, 10, 5, 0] = np.inf
+    dirty = _bwd_grads(fa, q, k, v, dy, ws, st, pad, torch.bfloat16, path)
+    inwin = torch.zeros((W, H), dtype=torch.bool, device="cuda")
+    inwin[4:11, 4:11] = True
+    for c, g, nm in zip(clean, dirty, ("dq", "dk", "dv")):
+        out = ~inwin
+        assert torch.equal(c[out].view(torch.int16), g[out].view(torch.int16)), f"path {path} {nm} changed outside"
+
+
+def test_windowed_backward_strip_full_size(fa):
+    """configs[2] at B = 32 runs the strip backward by default: the oracle on two images."""
+    W = H = 128
+    B, d = 32, 64
+    g = torch.Generator(device="cuda").manual_seed(10)
+    q, k, v, dy = (fa.jl_tensor(torch.randn((W, H, d, B), generator=g, device="cuda"), torch.bfloat16)
+                   for _ in range(4))
+    y, l, m = fa.windowed_fa(q, k, v, 7)
+    dq, dk, dvv = fa.windowed_fa_backward(q, k, v, y, dy, l, m, 7)
+    torch.cuda.synchronize()
+    for b in (0, 31):
+        sl = lambda t: _np(t[..., b:b + 1])
+        ref = O.windowed_fa_backward(sl(q), sl(k), sl(v), sl(dy), 7, 7, 3)
+        for a, b_, nm in zip((dq, dk, dvv), ref, ("dq", "dk", "dv")):
+            x = sl(a)
+            err = np.abs(x - b_).max() / max(np.abs(b_).max(), 1e-2)
+            assert np.all(np.isfinite(x)) and err <= 2e-2, f"image {b} {nm}: {err:.2e}"

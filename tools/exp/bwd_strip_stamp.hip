@@ -1,0 +1,37 @@
+// Phase timestamps of the strip windowed backward (win_bwd_strip) at configs[2]
+// geometry: the product source included with FA_STAMP defined.  Phases:
+// 0 entry, 1 first load landed, 2 phase A (dPᵀ, Sᵀ) done, 3 P / D / dS done,
+// 4 dQ stored, 5 end (dK, dV stored).  Diagnostic only (never shipped);
+// build / run: tools/exp/bwd_strip_stamp.py.
+#include <hip/hip_runtime.h>
+__device__ unsigned long long g_stamp_buf[8 * 16384];
+#define FA_STAMP(k)                                                                        \
+    do {                                                                                   \
+        if (threadIdx.x == 0) {                                                            \
+            ::g_stamp_buf[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime();            \
+            if ((k) == 0) ::g_stamp_buf[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime(); \
+            if ((k) == 5) ::g_stamp_buf[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                  \
+    } while (0)
+#include "../../flashattention.jl_amd/csrc/fa_windowed.hip"
+
+extern "C" int bwd_stamp_run(const void* q, const void* k, const void* v, const void* y, const void* dy, float* l,
+                             float* m, void* dq, void* dk, void* dv, int B, int mode, unsigned long long* host_out,
+                             int nwg_max) {
+    fa::WindowedBwdArgs a{};
+    a.dtype = FA_DTYPE_BF16; a.q = q; a.k = k; a.v = v; a.y = y; a.dy = dy; a.l = l; a.m = m;
+    a.dq = dq; a.dk = dk; a.dv_ = dv;
+    a.g.nsp = 2; a.g.S[0] = 128; a.g.S[1] = 128; a.g.S[2] = 1;
+    a.g.ws = 7; a.g.stride = 7; a.g.pad = 3;
+    a.g.O[0] = 19; a.g.O[1] = 19; a.g.O[2] = 1; a.g.T = 49; a.g.L = 361; a.g.P = 128 * 128;
+    a.d = 64; a.dv = 64; a.batch = B; a.scale = 0.125f;
+    fa::g_win_force_composed = mode;
+    const char* why = nullptr;
+    int rc = fa::windowed_bwd_rows<fa::bf16>(a, nullptr, &why);
+    fa::g_win_force_composed = 0;
+    if (rc != 0) return 1;
+    if (!host_out) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return 2;
+    if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamp_buf), sizeof(unsigned long long) * 8 * nwg_max) != hipSuccess) return 3;
+    return 0;
+}

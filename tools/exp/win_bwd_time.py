@@ -16,6 +16,6 @@ for B in [int(x) for x in (sys.argv[1:] or ["1", "8", "32"])]:
     y, lw, mw = fa_hip.windowed_fa(q, k, v, 7)
     tf = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), 50)
     tb = time_graph(lambda: fa_hip.windowed_fa_backward(q, k, v, y, dy, lw, mw, 7), 20)
-    # algorithmic bytes of the backward: q, k, v, y, dy read, dq, dk, dv written (bf16) + l, m
-    byt = B * (8 * 128 * 128 * 64 * 2 + 2 * 49 * 361 * 4)
+    # algorithmic bytes of the backward: q, k, v, dy read, dq, dk, dv written (bf16) + l, m (y not needed)
+    byt = B * (7 * 128 * 128 * 64 * 2 + 2 * 49 * 361 * 4)
     print(f"B={B:3d}: fwd {tf*1e6:8.1f} us   bwd {tb*1e6:8.1f} us  ({byt/tb/1e9:6.0f} GB/s algorithmic)", flush=True)
