@@ -1232,18 +1232,6 @@ struct FusedPlan {
     int nkb = 0, nqt = 0, xcd = 0;
     size_t flag_bytes = 0, bytes = 0;
 };
-// CUs of the device the work runs on: the stream's device (the current device for
-// the NULL stream, and for fa_dense_bwd_workspace, which takes no stream).
-static int device_cus(hipStream_t s) {
-    int dev = 0, cus = 0;
-    if (s != nullptr) {
-        if (hipStreamGetDevice(s, &dev) != hipSuccess) return 0;
-    } else if (hipGetDevice(&dev) != hipSuccess) {
-        return 0;
-    }
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    return cus;
-}
 static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch,
                             hipStream_t s = nullptr) {
     FusedPlan f;

@@ -100,6 +100,19 @@ int dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes, hipS
 int launch_dense_fwd_f64(const DenseArgs& a, hipStream_t s, const char** why);
 int launch_f64_bwd_stats(const DenseBwdArgs& a, double* nD, double* nlse, hipStream_t s, const char** why);
 // element size of a fa_dtype (0: unknown)
+// CUs of the device the work runs on: the stream's device (the current device for
+// the NULL stream, and for fa_dense_bwd_workspace, which takes no stream); 0 on error.
+inline int device_cus(hipStream_t s) {
+    int dev = 0, cus = 0;
+    if (s != nullptr) {
+        if (hipStreamGetDevice(s, &dev) != hipSuccess) return 0;
+    } else if (hipGetDevice(&dev) != hipSuccess) {
+        return 0;
+    }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return cus;
+}
+
 inline size_t dtype_size(int dtype) { return dtype == 0 ? 4 : dtype == 1 || dtype == 2 ? 2 : dtype == 3 ? 8 : 0; }
 size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch);

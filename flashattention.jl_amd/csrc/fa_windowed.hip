@@ -29,11 +29,15 @@
 #ifndef FA_STAMP
 #define FA_STAMP(k)
 #endif
+#ifndef FA_BSTAMP   // the persistent strip backward's per-strip hook: 0 start, 1 + j load j landed,
+                    // 9 + c dV chunk c, 11 + c dK chunk c, 13 + c dQ chunk c stored, 15 end
+#define FA_BSTAMP(k)
+#endif
 // Timing-only ablations of win_rows1s (tools/exp/win_ablate.hip; 0 in the product):
 // 1 = no y stores, 2 = every row load from one address; of win_strip
 // (tools/exp/strip_stamp.py): 4 = no y strip-image writes, 8 = no y global stores,
 // 16 = no 2-B stores of the chunks shared with a neighbour strip; of win_bwd_strip
-// (tools/exp/bwd_strip_stamp.py): 32 = no gradient stores
+// (tools/exp/bwd_strip_stamp.py): 32 = no gradient stores, 64 = no gradient image writes
 #ifndef FA_WIN_ABL
 #define FA_WIN_ABL 0
 #endif
@@ -1248,6 +1252,26 @@ __global__ __launch_bounds__(256 * NW, 8) void win_dma(const T* __restrict__ q, 
 //   V    : slot-row position c ^ ((f >> 3) & 1), window position w ^ (f & 7)  (ds_read_b128, conflict-free).
 // --------------------------------------------------------------------------
 constexpr int kStripW = 8;                          // windows per strip workgroup
+// Strip image [f][8 rows][64 px] (1 KB per feature): byte offset of pixel px.  The
+// 16-B chunk index is XORed with (row >> 1, f >> 2) so that the per-slot 2-B writes
+// of a wave (4 slot rows x 8 pixels x features f, f + 4) spread over 32 banks; the
+// 16-B chunk reads of the stores stay conflict-free.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// two fp32 -> a packed pair of T (v_cvt_pk_*), and back
+template <class T>
+__device__ __forceinline__ unsigned pk2(f32x2 v) {
+    typedef T T2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, T2));
+}
+template <class T>
+__device__ __forceinline__ f32x2 unpk2(unsigned u) {
+    typedef T T2 __attribute__((ext_vector_type(2)));
+    return __builtin_convertvector(__builtin_bit_cast(T2, u), f32x2);
+}
+__device__ __forceinline__ int simg_swz(int f, int row) { return ((row >> 1) & 3) | (((f >> 2) & 1) << 2); }
+__device__ __forceinline__ int simg_pos(int f, int row, int px) {
+    return f * 1024 + row * 128 + (((px >> 3) ^ simg_swz(f, row)) << 4) + (px & 7) * 2;
+}
 __device__ __forceinline__ int sqk_pos(int f, int c, int w) {   // byte offset in a Q / K chunk image
     return f * 1024 + c * 128 + ((w ^ ((f & 3) | (((c >> 1) & 1) << 2))) << 4);
 }
@@ -1472,7 +1496,7 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
                 const int px = ax + qtx - X0;
 #pragma unroll
                 for (int x = 0; x < 16; ++x)
-                    *(T*)(img + acc_row(x, h) * 1024 + qty * 128 + px * 2) = (T)(oa[qb][x] * inv);
+                    *(T*)(img + simg_pos(acc_row(x, h), qty, px)) = (T)(oa[qb][x] * inv);
             }
         }
         lds_barrier();
@@ -1483,7 +1507,7 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
             const int y = y0 + row, fg = vc * 32 + f, x0 = X0 + 8 * j;
             if (row >= ws || y < 0 || y >= H_ || fg >= dv || x0 + 8 <= xlo || x0 >= xhi || (FA_WIN_ABL & 8)) continue;
             const int go = ((fg * P_ + y * W_ + x0) * 2);
-            const char* src = img + f * 1024 + row * 128 + j * 16;
+            const char* src = img + f * 1024 + row * 128 + ((j ^ simg_swz(f, row)) << 4);
             if (x0 >= xlo && x0 + 8 <= xhi) {
                 __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)src, ors, go, 0, 0);
             } else if (!(FA_WIN_ABL & 16)) {             // a chunk shared with the neighbour strip
@@ -1972,285 +1996,230 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
 // geometry, rotated slots and swizzled LDS-DMA images as win_strip; every
 // gradient leaves as whole 16-B chunks of the strip's pixels.
 //
-//   phase A  (16-feature chunks, Sᵀ-style images): dPᵀ = V·dOᵀ, then Sᵀ = K·Qᵀ,
-//            keys on accumulator rows, queries on lanes, as in the forward;
-//            P = exp(τS − lse) from the forward's (l, m), read by a dword DMA;
-//            D = rowsum(P ∘ dP) in-lane (= rowsum(dO ∘ y): y is never read);
-//            dS = P ∘ (dP − D).  P and dS become bf16 B fragments (n = query).
-//   phase B  (32-feature chunks, row images), one output chunk per load:
-//            dQᵀ = τ Kᵀ dSᵀ straight from the fragments; Pᵀ and dSᵀ with keys
-//            on lanes by an identity MFMA (C = A·I with the fragments as A:
-//            exact, no LDS round trip); dKᵀ = τ Qᵀ dS, dVᵀ = dOᵀ P.  Each output
-//            chunk is written as a strip image [32 f][8 rows][64 px] over the
-//            chunk just read and stored as 16-B chunks.
-//   loads    : a ring of four 32-KB buffers, three loads in flight behind the
-//            one being read (counted vmcnt over the DMAs; the gradient stores
-//            in between only make a wait stronger), LDS-only barriers.
-// Keys / queries outside the window (slot row >= ws, columns outside [c0, c1),
-// rows outside the image) are masked to P = dS = 0 by selects, so a non-finite
-// neighbour pixel never enters this window's sums.
+//   phase A  (16-feature chunks, Sᵀ-style images): Sᵀ = K·Qᵀ, keys on accumulator
+//            rows, queries on lanes, as in the forward; P = exp(τS − lse) from the
+//            forward's (l, m) (read by a dword DMA) as bf16 B fragments (n = query)
+//            while the dO / V chunks land; then dPᵀ = V·dOᵀ in the same
+//            accumulators; D = rowsum(P ∘ dP) in-lane (= rowsum(dO ∘ y): y is
+//            never read); τ dS = τ P ∘ (dP − D) as bf16 B fragments.  The phase-B
+//            A operands of K and Q (lane = feature) are read from the same images
+//            into registers, so the strip's data is loaded from HBM once.
+//   phase B  (no loads): Pᵀ and dSᵀ with keys on lanes by an identity MFMA
+//            (C = A·I with the fragments as A: exact, no LDS round trip);
+//            dVᵀ = dOᵀ P (dO rows from the (dO, V) images, still in the ring),
+//            dKᵀ = Qᵀ (τ dS), dQᵀ = Kᵀ (τ dS)ᵀ, 32 output features at a time, each
+//            written as a 16-feature strip image [16 f][8 rows][64 px] (twice) and
+//            stored as whole 16-B chunks.
+//   loads    : a ring of four 32-KB buffers refilled as soon as a slot is read
+//            (Q / K slots at once, dO / V slots after dV), continuing into the
+//            next strip (persistent: one workgroup per CU over consecutive
+//            strips); exact vmcnt counts (loads, DMAs and stores retire in order);
+//            LDS-only barriers.
+// Keys / queries outside the window (slot row >= ws, columns outside [c0, c1))
+// are masked (K / V fragments zeroed, -inf exponent bias, selects on the query
+// lanes), so a non-finite neighbour pixel never enters this window's sums.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void wait_vm(int n) {   // n: a constant once the step loops are unrolled
+#define FA_VM_CASE(N) \
+    case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+__device__ __forceinline__ void wait_vm(int n) {   // n: even, 0 .. 46 (anything else waits for all)
     switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        FA_VM_CASE(0) FA_VM_CASE(2) FA_VM_CASE(4) FA_VM_CASE(6) FA_VM_CASE(8) FA_VM_CASE(10) FA_VM_CASE(12)
+        FA_VM_CASE(14) FA_VM_CASE(16) FA_VM_CASE(18) FA_VM_CASE(20) FA_VM_CASE(22) FA_VM_CASE(24) FA_VM_CASE(26)
+        FA_VM_CASE(28) FA_VM_CASE(30) FA_VM_CASE(32) FA_VM_CASE(34) FA_VM_CASE(36) FA_VM_CASE(38) FA_VM_CASE(40)
+        FA_VM_CASE(42) FA_VM_CASE(44) FA_VM_CASE(46)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
+#undef FA_VM_CASE
 
-// The strip image [32 f][8 rows][64 px] (pixel X0 + px) of output features
-// fbase .. fbase + 31 as 16-B chunk stores; chunks that straddle the strip ends
-// (only when no first-strip width aligns them) as 2-B stores.
-template <class T>
-__device__ __forceinline__ void strip_store(const char* img, __amdgpu_buffer_rsrc_t ors, int tid, int fbase, int C,
-                                            int y0, int ws, int H_, int W_, int P_, int X0, int xlo, int xhi) {
+// Per-lane store plan of a 16-feature strip image, fixed for the strip: unit
+// u = it * 512 + tid (it = 0, 1) is (feature it * 8 + (tid >> 6), row (tid >> 3) & 7,
+// 16-B chunk tid & 7); the two units differ by constants.
+struct StripStore {
+    int go0;          // byte offset of the unit's chunk in the slab, feature 0
+    int roff;         // LDS byte offset of unit 0 in the image
+    bool full;        // a whole in-image 16-B chunk
+    bool part;        // straddles a strip end (2-B stores; only when the ends are unaligned)
+    int e0, e1;       // the straddling chunk's pixels inside the strip: [e0, e1)
+};
+__device__ __forceinline__ StripStore strip_store_plan(int tid, int y0, int ws, int H_, int W_, int X0, int xlo, int xhi) {
+    const int f = tid >> 6, row = (tid >> 3) & 7, j = tid & 7;
+    const int y = y0 + row, x0 = X0 + 8 * j;
+    const bool rok = row < ws && y >= 0 && y < H_ && x0 + 8 > xlo && x0 < xhi;
+    StripStore p;
+    p.full = rok && x0 >= xlo && x0 + 8 <= xhi;
+    p.part = rok && !p.full;
+    p.go0 = (y * W_ + x0) * 2;                       // + feature * P * 2 at the store
+    p.roff = f * 1024 + row * 128 + ((j ^ simg_swz(f, row)) << 4);
+    p.e0 = max(xlo - x0, 0);
+    p.e1 = min(xhi - x0, 8);
+    return p;
+}
+
+// A 16-feature strip image [16 f][8 rows][64 px] (simg_pos) of output features
+// fbase .. fbase + 15 as 16-B chunk stores, 2 per lane (invalid lanes get an
+// out-of-range offset: the store is dropped); chunks straddling a strip end as
+// 2-B stores (PARTIAL only).
+template <class T, bool PARTIAL>
+__device__ __forceinline__ void strip_store16(const char* img, __amdgpu_buffer_rsrc_t ors, const StripStore& sp, int tid,
+                                              int fbase, int C, int P_) {
     if (FA_WIN_ABL & 32) return;
-    u32x4 val[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) val[it] = lds_b128(img + (it * 512 + tid) * 16);   // unit u at byte 16 u
+    const int f = tid >> 6;
+    u32x4 val[2];
+    const uint32_t ra = lds_off(img) + sp.roff;      // unit 1: + 8 KB
+    asm volatile("ds_read_b128 %0, %1" : "=v"(val[0]) : "v"(ra) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:8192" : "=v"(val[1]) : "v"(ra) : "memory");
     lds_wait();
+    lds_fence(val[0]);
+    lds_fence(val[1]);
 #pragma unroll
-    for (int it = 0; it < 4; ++it) lds_fence(val[it]);
+    for (int it = 0; it < 2; ++it) {
+        const int fg = fbase + it * 8 + f;
+        const bool ok = fg < C && sp.full;
+        __builtin_amdgcn_raw_buffer_store_b128(val[it], ors, ok ? sp.go0 + fg * P_ * 2 : 0x7FFFFFF0, 0, 0);
+    }
+    if (PARTIAL && sp.part) {                        // only when some strip end is not on a 16-B chunk
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int u = it * 512 + tid, f = u >> 6, row = (u >> 3) & 7, j = u & 7;
-        const int y = y0 + row, fg = fbase + f, x0 = X0 + 8 * j;
-        if (row >= ws || y < 0 || y >= H_ || fg >= C || x0 + 8 <= xlo || x0 >= xhi) continue;
-        const int go = (fg * P_ + y * W_ + x0) * 2;
-        if (x0 >= xlo && x0 + 8 <= xhi) {
-            __builtin_amdgcn_raw_buffer_store_b128(val[it], ors, go, 0, 0);
-        } else {
+        for (int it = 0; it < 2; ++it) {
+            const int fg = fbase + it * 8 + f;
+            if (fg >= C) continue;
+            const int go = sp.go0 + fg * P_ * 2;
             for (int e = 0; e < 8; ++e)
-                if (x0 + e >= xlo && x0 + e < xhi)
+                if (e >= sp.e0 && e < sp.e1)
                     __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(val[it][e >> 1] >> (16 * (e & 1))), ors,
                                                           go + 2 * e, 0, 0);
         }
     }
 }
 
-template <class T, int D, int DV>
+// 8 accumulator values (registers X0 .. X0 + 7: features acc_row(x, h) - 16 (X0 / 8) of one
+// slot) into a 16-feature strip image at base (= simg_pos(4h, row, px)): the feature offsets
+// are immediates (the swizzle depends on feature bit 2 = h only); pairs share one conversion.
+template <class T, int X0, int X = X0>
+__device__ __forceinline__ void img_w8(uint32_t base, const f32x16& acc) {
+    if constexpr (X < X0 + 8) {
+        typedef T T2 __attribute__((ext_vector_type(2)));
+        typedef float F2 __attribute__((ext_vector_type(2)));
+        const T2 pr = __builtin_convertvector((F2){acc[X], acc[X + 1]}, T2);
+        const unsigned u = __builtin_bit_cast(unsigned, pr);
+        constexpr int f0 = (X & 3) + 8 * (X >> 2) - 2 * X0, f1 = ((X + 1) & 3) + 8 * ((X + 1) >> 2) - 2 * X0;
+        asm volatile("ds_write_b16 %0, %1 offset:%2" : : "v"(base), "v"(u), "i"(f0 * 1024) : "memory");
+        asm volatile("ds_write_b16_d16_hi %0, %1 offset:%2" : : "v"(base), "v"(u), "i"(f1 * 1024) : "memory");
+        img_w8<T, X0, X + 2>(base, acc);
+    }
+}
+
+struct StripPos {                                    // one strip: batch slab, window row, first window
+    int b, wy, y0, wx0, nvalid;
+};
+
+template <class T, int D, int DV, bool PARTIAL>
 __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q, const T* __restrict__ k,
                                                         const T* __restrict__ v, const T* __restrict__ dy,
                                                         const float* __restrict__ lw, const float* __restrict__ mw,
                                                         T* __restrict__ dq, T* __restrict__ dk, T* __restrict__ dvo,
-                                                        WinDev g, int d, int dv, int nsx, int k0, int nwg,
-                                                        float scale, float scale_log2) {
+                                                        WinDev g, int d, int dv, int nsx, int k0, int nstrip,
+                                                        int per, float scale, float scale_log2) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
     static_assert(D % 32 == 0 && D <= 64 && DV % 32 == 0 && DV <= 64, "head dims");
-    constexpr int NOV = DV / 16, NA = NOV + D / 16;   // phase A loads: (dO, V), then (Q, K) 16-feature chunks
-    constexpr int NBK = D / 32, NBQ = D / 32, NBO = DV / 32;
-    constexpr int NL = NA + NBK + NBQ + NBO;          // phase B loads: K (dQ), Q (dK), dO (dV) 32-feature chunks
-    constexpr int R = 4, BUF = 32768;
-    __shared__ __attribute__((aligned(16))) char smem[R * BUF + 2 * 8 * 64 * 4];
-    float* const ls = (float*)(smem + R * BUF);       // l, m of the strip's windows: [window][64]
-    float* const ms = ls + 8 * 64;
+    constexpr int NQK = D / 16, NOV = DV / 16, NA = NQK + NOV;   // loads: (Q, K), then (dO, V) 16-feature chunks
+    constexpr int NC = D / 32, NCV = DV / 32;        // 32-feature output chunks of dQ / dK and of dV
+    constexpr int R = 4, BUF = 32768, IMG = 16384;
+    static_assert(NA >= R, "every ring slot is a load of the strip");
+    __shared__ __attribute__((aligned(16))) char smem[R * BUF + IMG + 2 * 2 * 8 * 64 * 4];
+    char* const img = smem + R * BUF;                // 16-feature gradient image
+    float* const lms = (float*)(img + IMG);          // l, m of a strip's windows: [parity][l | m][window][64]
 
-    FA_STAMP(0);
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // lane-derived values are re-derived from an opaque copy of threadIdx.x in every strip
+    // iteration: hoisted out of the loop, their many per-lane addresses would stay live and spill
+    int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride, nwx = g.O[0];
-    const int lid = xcd_remap(blockIdx.x, nwg);
-    const int sxi = lid % nsx, t0 = lid / nsx, wy = t0 % g.O[1], b = t0 / g.O[1];
-    const int wx0 = sxi == 0 ? 0 : k0 + (sxi - 1) * kStripW, y0 = wy * st - g.pad;
-    const int nvalid = min(sxi == 0 ? k0 : kStripW, nwx - wx0);
-    auto ax_of = [&](int w) __attribute__((always_inline)) { return min(max(((wx0 + w) * st - g.pad) & ~1, 0), W_ - 8); };
-    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
-    const auto ors = slab_rsrc(dy + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
-    const int64_t wrow = (int64_t)g.T * ((int64_t)nwx * wy + (int64_t)g.L * b);   // l, m of window (0, wy)
-    const auto lrs = slab_rsrc(lw + wrow, (uint32_t)(g.T * nwx * 4));
-    const auto mrs = slab_rsrc(mw + wrow, (uint32_t)(g.T * nwx * 4));
-
-    // one DMA instruction = one feature row fl of an image: lane -> (slot row, window)
-    auto dma_qk = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg, int C) __attribute__((always_inline)) {   // Sᵀ-style image (tr reads)
+    auto pos_of = [&](int sid) __attribute__((always_inline)) {
+        const int sxi = sid % nsx, t0 = sid / nsx;
+        StripPos p;
+        p.wy = t0 % g.O[1];
+        p.b = t0 / g.O[1];
+        p.wx0 = sxi == 0 ? 0 : k0 + (sxi - 1) * kStripW;
+        p.y0 = p.wy * st - g.pad;
+        p.nvalid = min(sxi == 0 ? k0 : kStripW, nwx - p.wx0);
+        return p;
+    };
+    auto ax_of = [&](const StripPos& p, int w) __attribute__((always_inline)) {
+        return min(max(((p.wx0 + w) * st - g.pad) & ~1, 0), W_ - 8);
+    };
+    // one DMA instruction = one feature row fl of an Sᵀ-style image: lane -> (slot row, window)
+    auto dma_qk = [&](const StripPos& p, __amdgpu_buffer_rsrc_t rs, char* im, int fl, int fg, int C)
+        __attribute__((always_inline)) {
         const int pc = lane >> 3, pw = lane & 7;
-        const int w = pw ^ ((fl & 3) | (((pc >> 1) & 1) << 2)), y = y0 + pc;
-        const bool ok = w < nvalid && pc < ws && y >= 0 && y < H_ && fg < C;
-        const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
+        const int w = pw ^ ((fl & 3) | (((pc >> 1) & 1) << 2)), y = p.y0 + pc;
+        const bool ok = w < p.nvalid && pc < ws && y >= 0 && y < H_ && fg < C;
+        const int off = ok ? (fg * P_ + y * W_ + ax_of(p, w)) * 2 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(im + fl * 1024), 16,
                                                  off, 0, 0, 0);
     };
-    auto dma_row = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg, int C) __attribute__((always_inline)) {  // row image (16-B / 8-B reads)
-        const int c = (lane >> 3) ^ ((fl >> 3) & 1), w = (lane & 7) ^ (fl & 7), y = y0 + c;
-        const bool ok = w < nvalid && c < ws && y >= 0 && y < H_ && fg < C;
-        const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
-                                                 off, 0, 0, 0);
+    // VMEM instructions this wave has issued (loads, DMAs, counted stores), and the count
+    // right after each ring slot's load: the wait for a slot is vmcnt(issued - mark)
+    // (loads, stores and DMA retire in issue order: MI355X_MICROARCH, vmcnt).  Slots are
+    // runtime values (a strip's NA loads need not be a multiple of R), so the marks are
+    // four scalars, not an array (which would go to scratch).
+    int vm_issued = 0;
+    int mark0 = 0, mark1 = 0, mark2 = 0, mark3 = 0;
+    auto mark_of = [&](int slot) __attribute__((always_inline)) {
+        return slot == 0 ? mark0 : slot == 1 ? mark1 : slot == 2 ? mark2 : mark3;
     };
-    // load j into buffer j % R: 32 DMA instructions (one feature row each), 4 per wave
-    auto issue = [&](__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr,
-                     __amdgpu_buffer_rsrc_t orr, int j) __attribute__((always_inline)) {
-        char* buf = smem + (j % R) * BUF;
+    // load j of strip p into ring slot `slot`: 32 DMA instructions (one feature row each), 4 per
+    // wave; a strip's l, m (2 DMA instructions per wave, into parity par) right after its load 0
+    auto issue = [&](const StripPos& p, int j, int slot, int par) __attribute__((always_inline)) {
+        char* buf = smem + slot * BUF;
+        const int64_t bo = (int64_t)p.b;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int rr = i * 8 + wave;                 // 0..31
-            if (j < NOV) {
-                if (rr < 16) dma_qk(orr, buf, rr, j * 16 + rr, dv);
-                else dma_qk(vr, buf + 16384, rr - 16, j * 16 + rr - 16, dv);
-            } else if (j < NA) {
-                if (rr < 16) dma_qk(qr, buf, rr, (j - NOV) * 16 + rr, d);
-                else dma_qk(kr, buf + 16384, rr - 16, (j - NOV) * 16 + rr - 16, d);
-            } else if (j < NA + NBK) {
-                dma_row(kr, buf, rr, (j - NA) * 32 + rr, d);
-            } else if (j < NA + NBK + NBQ) {
-                dma_row(qr, buf, rr, (j - NA - NBK) * 32 + rr, d);
+            if (j < NQK) {
+                if (rr < 16) dma_qk(p, slab_rsrc(q + bo * d * P_, (uint32_t)(d * P_ * 2)), buf, rr, j * 16 + rr, d);
+                else dma_qk(p, slab_rsrc(k + bo * d * P_, (uint32_t)(d * P_ * 2)), buf + 16384, rr - 16,
+                            j * 16 + rr - 16, d);
             } else {
-                dma_row(orr, buf, rr, (j - NA - NBK - NBQ) * 32 + rr, dv);
+                if (rr < 16) dma_qk(p, slab_rsrc(dy + bo * dv * P_, (uint32_t)(dv * P_ * 2)), buf, rr,
+                                    (j - NQK) * 16 + rr, dv);
+                else dma_qk(p, slab_rsrc(v + bo * dv * P_, (uint32_t)(dv * P_ * 2)), buf + 16384, rr - 16,
+                            (j - NQK) * 16 + rr - 16, dv);
             }
         }
-    };
-    {   // l, m of this wave's window (64 dwords per window, lanes >= T read 0), ahead of load 0
-        const int w = wave;
-        const int off = (w < nvalid && lane < g.T) ? (g.T * (wx0 + w) + lane) * 4 : 0x7FFFFFF0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (__attribute__((address_space(3))) void*)(ls + w * 64), 4, off,
-                                                 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(mrs, (__attribute__((address_space(3))) void*)(ms + w * 64), 4, off,
-                                                 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < R; ++j) issue(qrs, krs, vrs, ors, j);
-
-    // ---- this wave's window ----
-    const int wl = wave;
-    const bool wok = wl < nvalid;
-    const int wx = wx0 + wl, xs = wx * st - g.pad, ax = ax_of(wl);
-    const int c0 = xs - ax, c1 = c0 + ws;
-    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-    auto slot_ok = [&](int s) __attribute__((always_inline)) {                          // slot s of this window: a real token of the image
-        const int sx = s & 7, sy = s >> 3;
-        return wok && sy < ws && sx >= c0 && sx < c1 && y0 + sy >= 0 && y0 + sy < H_;
-    };
-    // step j: wait for load j (the loads issued after it stay in flight), LDS barrier
-    auto step_wait = [&](int j) __attribute__((always_inline)) {
-        wait_vm(4 * min(R - 1, NL - 1 - j));
-        lds_barrier();
-    };
-
-    f32x16 sa[2][2], pa[2][2];                           // Sᵀ, dPᵀ: [key block][query block]
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) sa[kb][qb][x] = pa[kb][qb][x] = 0.0f;
-
-    // ---- phase A ----
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        step_wait(j);
-        if (j == 0) FA_STAMP(1);
-        const char* buf = smem + (j % R) * BUF;
-        s16x4 rk[2][2], rq[2][2];                        // keys (V / K, permuted), queries (dO / Q)
-#pragma unroll
-        for (int blk = 0; blk < 2; ++blk) {
-            const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
-            rk[blk][0] = lds_tr16(a);
-            rk[blk][1] = lds_tr16(a + 4 * 1024);
-            const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
-            rq[blk][0] = lds_tr16(aq);
-            rq[blk][1] = lds_tr16(aq + 4 * 1024);
-        }
-        lds_wait();
-        F8 kf[2], qf[2];
-#pragma unroll
-        for (int blk = 0; blk < 2; ++blk) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) { lds_fence(rk[blk][i]); lds_fence(rq[blk][i]); }
-            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rk[blk][0]), __builtin_bit_cast(F4, rk[blk][1]),
-                                              0, 1, 2, 3, 4, 5, 6, 7);
-            qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rq[blk][0]), __builtin_bit_cast(F4, rq[blk][1]),
-                                              0, 1, 2, 3, 4, 5, 6, 7);
-        }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb) {
-                if (j < NOV) pa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], pa[kb][qb]);
-                else sa[kb][qb] = mfma32x32x16(kf[kb], qf[qb], sa[kb][qb]);
-            }
-        if (j + R < NL) {
-            lds_barrier();                               // every wave is done with this buffer
-            issue(qrs, krs, vrs, ors, j + R);
-        }
-    }
-    FA_STAMP(2);
-
-    // ---- P, D, dS per query (lane) ----
-    F8 pf[2][2][2], dsf[2][2][2];                        // [query block][key block][16-key half]
-    float lq[2], mq[2];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-        const int qs = qb * 32 + r;
-        const int tq = slot_ok(qs) ? (qs >> 3) * ws + (qs & 7) - c0 : 0;   // window token of the query slot
-        lq[qb] = lds_b32(ls + wl * 64 + tq);
-        mq[qb] = lds_b32(ms + wl * 64 + tq);
-    }
-    lds_wait();
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-        lds_fence(lq[qb]);
-        lds_fence(mq[qb]);
-        const int qs = qb * 32 + r;
-        const bool qv = slot_ok(qs);
-        const float nl = qv ? (mq[qb] + __logf(lq[qb])) * kLog2e : 0.0f;
-        float dsum = 0.0f;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
-                const bool ok = qv && slot_ok(kt);
-                const float pr = ok ? exp2_fast(fmaf(sa[kb][qb][x], scale_log2, -nl)) : 0.0f;
-                sa[kb][qb][x] = pr;
-                pa[kb][qb][x] = ok ? pa[kb][qb][x] : 0.0f;
-                dsum = fmaf(pr, pa[kb][qb][x], dsum);
-            }
-        const float Dq = swap_halves_sum(dsum);
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                pf[qb][kb][x >> 3][x & 7] = (T)sa[kb][qb][x];
-                dsf[qb][kb][x >> 3][x & 7] = (T)(sa[kb][qb][x] * (pa[kb][qb][x] - Dq));
-            }
-    }
-    FA_STAMP(3);
-
-    // ---- phase B ----
-    const int xs0 = wx0 * st - g.pad, X0 = xs0 & ~7;     // strip start, its 16-B aligned base
-    const int xlo = max(xs0, 0), xhi = min(xs0 + nvalid * ws, W_);
-    const auto dqs = slab_rsrc(dq + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto dks = slab_rsrc(dk + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto dvs = slab_rsrc(dvo + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
-    unsigned cm[4];                                      // slot-column mask of a 16-B row fragment
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        cm[j] = ((2 * j >= c0 && 2 * j < c1) ? 0x0000FFFFu : 0u) | ((2 * j + 1 >= c0 && 2 * j + 1 < c1) ? 0xFFFF0000u : 0u);
-    // write a 32 x 32 block (features on accumulator rows, slot s on the lane) into the strip image
-    auto img_write = [&](char* img, const f32x16& acc, float mul, int s) __attribute__((always_inline)) {
-        if (slot_ok(s)) {
-            const int px = ax + (s & 7) - X0, row = s >> 3;
-#pragma unroll
-            for (int x = 0; x < 16; ++x)
-                lds_w16(img + acc_row(x, h) * 1024 + row * 128 + px * 2,
-                        __builtin_bit_cast(unsigned short, (T)(acc[x] * mul)));
+        vm_issued += 4;
+        mark0 = slot == 0 ? vm_issued : mark0;
+        mark1 = slot == 1 ? vm_issued : mark1;
+        mark2 = slot == 2 ? vm_issued : mark2;
+        mark3 = slot == 3 ? vm_issued : mark3;
+        if (j == 0) {
+            const int64_t wrow = (int64_t)g.T * ((int64_t)nwx * p.wy + (int64_t)g.L * p.b);   // window (0, wy)
+            const int off = (wave < p.nvalid && lane < g.T) ? (g.T * (p.wx0 + wave) + lane) * 4 : 0x7FFFFFF0;
+            float* dst = lms + par * 1024 + wave * 64;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(slab_rsrc(lw + wrow, (uint32_t)(g.T * nwx * 4)),
+                                                     (__attribute__((address_space(3))) void*)dst, 4, off, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(slab_rsrc(mw + wrow, (uint32_t)(g.T * nwx * 4)),
+                                                     (__attribute__((address_space(3))) void*)(dst + 512), 4, off, 0, 0,
+                                                     0);
+            vm_issued += 2;
         }
     };
-    // 16 query slots 16 s' + 4h + {0..3, 8..11} of block qb, feature r of a row image (the
-    // B-fragment order of an identity-transposed block), column-masked
-    // (asm reads: lds_wait + lds_fence before use)
-    auto frag_perm = [&](const char* buf, int qb, int s_, u32x2& lo, u32x2& hi) __attribute__((always_inline)) {
-        lo = lds_b64(buf + sv_pos(r, qb * 4 + 2 * s_, wl) + 8 * h);
-        hi = lds_b64(buf + sv_pos(r, qb * 4 + 2 * s_ + 1, wl) + 8 * h);
-    };
+
+    // strips [s0, s1) of this workgroup: consecutive strips, so every workgroup gets a mix
+    // of full, edge and bottom-row strips
+    int sid = blockIdx.x * per;
+    const int s1 = min(sid + per, nstrip);
+    StripPos cur = pos_of(sid);
+#pragma unroll
+    for (int j = 0; j < R; ++j) issue(cur, j, j, 0);
+    int gbase = 0;                                   // ring slot of the current strip's load 0
+
+    int g4, kh, qq, pp, sig;
+    const unsigned one = std::is_same<T, bf16>::value ? 0x3F80u : 0x3C00u;
     // one-hot B fragment: element e of lane (r, h) is 1 iff 16 s2 + 8 h + e == r
     auto ident = [&](int s2) __attribute__((always_inline)) {
         const int e = r - 16 * s2 - 8 * h;
-        const unsigned one = std::is_same<T, bf16>::value ? 0x3F80u : 0x3C00u;
         u32x4 u = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -2260,107 +2229,352 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
         return __builtin_bit_cast(F8, u);
     };
     const F8 id0 = ident(0), id1 = ident(1);
-    // transpose: block (kb, qb) of X (B fragments, queries on lanes) -> keys on lanes, then
-    // B fragments [key block][query block][s'] in frag_perm's query order
-    auto transpose = [&](const F8 (&xf)[2][2][2], F8 (&xt)[2][2][2]) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb) {
-                f32x16 c;
-#pragma unroll
-                for (int x = 0; x < 16; ++x) c[x] = 0.0f;
-                c = mfma32x32x16(xf[qb][kb][0], id0, c);
-                c = mfma32x32x16(xf[qb][kb][1], id1, c);
-#pragma unroll
-                for (int x = 0; x < 16; ++x) xt[kb][qb][x >> 3][x & 7] = (T)c[x];
-            }
-    };
-    auto step_end = [&](int j) __attribute__((always_inline)) {
-        if (j + R < NL) {
-            lds_barrier();                               // every wave has read the image
-            issue(qrs, krs, vrs, ors, j + R);
-        }
-    };
 
-    // dQᵀ = τ Kᵀ dSᵀ
+    for (int it = 0; sid < s1; ++it, ++sid) {
+        [[maybe_unused]] const int fa_sid = sid;
+        FA_BSTAMP(0);
+        tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        lane = tid & 63; r = lane & 31; h = lane >> 5;
+        g4 = lane >> 4; kh = g4 & 1; qq = (lane & 15) >> 2; pp = lane & 3;
+        sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
+        const bool has_next = sid + 1 < s1;
+        const StripPos nxt = has_next ? pos_of(sid + 1) : cur;
+        const int par = it & 1;
+        auto slot_of = [&](int j) __attribute__((always_inline)) { return (gbase + j) & (R - 1); };
+        // load j landed in every wave: its own DMA (counted wait), then the LDS barrier
+        auto step_wait = [&](int j) __attribute__((always_inline)) {
+            __builtin_amdgcn_sched_barrier(0);          // keep each step's work in its step (register pressure)
+            wait_vm(vm_issued - mark_of(slot_of(j)));
+            lds_barrier();
+            FA_BSTAMP(1 + j);
+        };
+        // ring slot of load j is free: issue the load R later in the stream (this strip's, or the next's)
+        auto refill = [&](int j) __attribute__((always_inline)) {
+            if (j + R < NA) issue(cur, j + R, slot_of(j), par);
+            else if (has_next) issue(nxt, j + R - NA, slot_of(j), par ^ 1);
+        };
+
+        // ---- this wave's window ----
+        const int wl = wave;
+        const bool wok = wl < cur.nvalid;
+        const int y0 = cur.y0, b = cur.b;
+        const int wx = cur.wx0 + wl, xs = wx * st - g.pad, ax = ax_of(cur, wl);
+        const int c0 = xs - ax, c1 = c0 + ws;
+        auto slot_ok = [&](int s) __attribute__((always_inline)) {   // slot s of this window: a real token of the image
+            const int sx = s & 7, sy = s >> 3;
+            return wok && sy < ws && sx >= c0 && sx < c1 && y0 + sy >= 0 && y0 + sy < H_;
+        };
+        // Masking.  Keys: the K / V fragments (A operands; lane = key) are zeroed per lane for
+        // keys outside the window (slot row >= ws or column outside [c0, c1)), so Sᵀ and dPᵀ are
+        // finite there whatever the neighbour pixels hold; P gets a -inf exponent bias for those
+        // keys: per column (register x & 7, wave-uniform) and per slot row (lane half, kb, x >> 3).
+        // Queries (lanes): P and dS are selected to 0 outside the window.  Rows outside the image
+        // are zero-padding tokens, as in the forward (P > 0, K = V = 0: no contribution).
+        bool qv[2];
 #pragma unroll
-    for (int c = 0; c < NBK; ++c) {
-        const int j = NA + c;
-        step_wait(j);
-        char* buf = smem + (j % R) * BUF;
-        f32x16 oa[2];
+        for (int qb = 0; qb < 2; ++qb) {
+            const int qs = qb * 32 + r;
+            qv[qb] = wok && (qs >> 3) < ws && (qs & 7) >= c0 && (qs & 7) < c1;
+        }
+        bool kfv[2];                                     // this lane's key (A row) of tr-read block blk: lane i of
+        {                                                // a 16-lane group receives column i, i.e. chunk qq
+            const int sq = (qq == 1) ? 2 : (qq == 2) ? 1 : qq;   // sig of the supplying lanes
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+            for (int blk = 0; blk < 2; ++blk) {
+                const int krow = 4 * blk + 2 * kh + (sq >> 1), kcol = 4 * (sq & 1) + (lane & 3);
+                kfv[blk] = krow < ws && kcol >= c0 && kcol < c1;
+            }
+        }
+        float colb[8], rowb[2][2];                       // 0 or -inf exponent bias
 #pragma unroll
-            for (int x = 0; x < 16; ++x) oa[qb][x] = 0.0f;
-        u32x4 kr[2][2];
+        for (int c = 0; c < 8; ++c) colb[c] = (c >= c0 && c < c1) ? 0.0f : kNegInf;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) kr[kb][s2] = lds_b128(buf + sv_pos(r, kb * 4 + s2 * 2 + h, wl));
-        lds_wait();
+            for (int x2 = 0; x2 < 2; ++x2) rowb[kb][x2] = (kb * 4 + 2 * x2 + h < ws) ? 0.0f : kNegInf;
+
+        f32x16 acc[2][2];                                // Sᵀ over the (Q, K) chunks, then dPᵀ: [key block][query block]
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                lds_fence(kr[kb][s2]);
+            for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) kr[kb][s2][i] &= cm[i];
+                for (int x = 0; x < 16; ++x) acc[kb][qb][x] = 0.0f;
+        F8 pf[2][2][2], dsf[2][2][2];                    // P, τ dS: [query block][key block][16-key half]
+        // phase-B A operands kept in registers (lane r = feature 32 c + r): K rows for dQ
+        // (8 consecutive keys of a slot row), Q rows for dK (the transposed fragments'
+        // query order 16 s' + 4h + {0..3, 8..11}); read from the phase-A images
+        u32x4 kst[NC][2][2];
+        u32x2 qlo[NC][2][2], qhi[NC][2][2];
+
+        // ---- phase A ----
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+            step_wait(j);
+            const char* buf = smem + slot_of(j) * BUF;
+            s16x4 rk[2][2], rq[2][2];                    // keys (K / V, permuted), queries (Q / dO)
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk) {
+                const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
+                rk[blk][0] = lds_tr16(a);
+                rk[blk][1] = lds_tr16(a + 4 * 1024);
+                const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
+                rq[blk][0] = lds_tr16(aq);
+                rq[blk][1] = lds_tr16(aq + 4 * 1024);
+            }
+            if (j < NQK) {                               // this chunk's 16 features of the K / Q stashes
+                const int c = j >> 1, fl = r & 15;
+                if ((r >> 4) == (j & 1)) {
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+                            kst[c][kb][s2] = lds_b128(buf + 16384 + sqk_pos(fl, kb * 4 + s2 * 2 + h, wl));
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                        for (int s_ = 0; s_ < 2; ++s_) {
+                            qlo[c][qb][s_] = lds_b64(buf + sqk_pos(fl, qb * 4 + 2 * s_, wl) + 8 * h);
+                            qhi[c][qb][s_] = lds_b64(buf + sqk_pos(fl, qb * 4 + 2 * s_ + 1, wl) + 8 * h);
+                        }
+                }
+            }
+            lds_wait();
+            if (j < NQK) {
+                const int c = j >> 1;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) lds_fence(kst[c][kb][s2]);
 #pragma unroll
                 for (int qb = 0; qb < 2; ++qb)
-                    oa[qb] = mfma32x32x16(__builtin_bit_cast(F8, kr[kb][s2]), dsf[qb][kb][s2], oa[qb]);
-            }
-        lds_barrier();                                   // every wave has read this K chunk
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) img_write(buf, oa[qb], scale, qb * 32 + r);
-        lds_barrier();
-        strip_store<T>(buf, dqs, tid, c * 32, d, y0, ws, H_, W_, P_, X0, xlo, xhi);
-        step_end(j);
-    }
-    FA_STAMP(4);
+                    for (int s_ = 0; s_ < 2; ++s_) { lds_fence(qlo[c][qb][s_]); lds_fence(qhi[c][qb][s_]); }
+            }
+            F8 kf[2], qf[2];
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) { lds_fence(rk[blk][i]); lds_fence(rq[blk][i]); }
+                u32x4 ku = __builtin_bit_cast(u32x4, __builtin_shufflevector(rk[blk][0], rk[blk][1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ku[i] = kfv[blk] ? ku[i] : 0u;
+                kf[blk] = __builtin_bit_cast(F8, ku);
+                qf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, rq[blk][0]), __builtin_bit_cast(F4, rq[blk][1]),
+                                                  0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) acc[kb][qb] = mfma32x32x16(kf[kb], qf[qb], acc[kb][qb]);
+            if (j < NQK) {                               // a Q / K slot is free at once; dO / V stay for dV
+                lds_barrier();
+                refill(j);
+            }
+            if (j == NQK - 1) {                          // Sᵀ complete: P = exp(τS − lse) (bf16), while dO / V load
+                const float* ls = lms + par * 1024 + wl * 64;
+                float lq[2], mq[2];
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) {
+                    const int qs = qb * 32 + r;
+                    const int tq = qv[qb] ? (qs >> 3) * ws + (qs & 7) - c0 : 0;   // window token of the query slot
+                    lq[qb] = lds_b32(ls + tq);
+                    mq[qb] = lds_b32(ls + 512 + tq);
+                }
+                lds_wait();
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) {
+                    lds_fence(lq[qb]);
+                    lds_fence(mq[qb]);
+                    const float nl = (mq[qb] + __logf(lq[qb])) * kLog2e;
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                        for (int x2 = 0; x2 < 2; ++x2) {
+                            const float nlb = nl - rowb[kb][x2];           // +inf on slot rows >= ws
+                            u32x4 pu;
+#pragma unroll
+                            for (int e = 0; e < 8; e += 2) {            // packed fp32: v_pk_fma / v_pk_add
+                                const int x = 8 * x2 + e;
+                                const f32x2 sv = {acc[kb][qb][x], acc[kb][qb][x + 1]};
+                                const f32x2 arg = __builtin_elementwise_fma(sv, (f32x2){scale_log2, scale_log2},
+                                                                            (f32x2){-nlb, -nlb}) +
+                                                  (f32x2){colb[e], colb[e + 1]};
+                                const f32x2 pr = {exp2_fast(arg[0]), exp2_fast(arg[1])};
+                                pu[e >> 1] = qv[qb] ? pk2<T>(pr) : 0u;
+                                acc[kb][qb][x] = acc[kb][qb][x + 1] = 0.0f;
+                            }
+                            pf[qb][kb][x2] = __builtin_bit_cast(F8, pu);
+                        }
+                }
+                // pin P here, under the dO / V loads (the optimizer would sink it to its first use)
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                        for (int x2 = 0; x2 < 2; ++x2) asm volatile("" : "+v"(pf[qb][kb][x2]));
+            }
+        }
 
-    // dKᵀ = τ Qᵀ dS, dVᵀ = dOᵀ P (keys on lanes)
+        // ---- D = rowsum(P ∘ dP), τ dS = τ P ∘ (dP − D) per query (lane) ----
 #pragma unroll
-    for (int c = 0; c < NBQ + NBO; ++c) {
-        const int j = NA + NBK + c;
-        const bool isk = c < NBQ;
-        F8 xt[2][2][2];
-        transpose(isk ? dsf : pf, xt);
-        step_wait(j);
-        char* buf = smem + (j % R) * BUF;
-        f32x16 oa[2];
+        for (int qb = 0; qb < 2; ++qb) {
+            f32x2 ds2 = {0.0f, 0.0f};
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+            for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int x = 0; x < 16; ++x) oa[kb][x] = 0.0f;
-        u32x2 lo[2][2], hi[2][2];
+                for (int x = 0; x < 16; x += 2)
+                    ds2 = __builtin_elementwise_fma(unpk2<T>(__builtin_bit_cast(u32x4, pf[qb][kb][x >> 3])[(x & 7) >> 1]),
+                                                    (f32x2){acc[kb][qb][x], acc[kb][qb][x + 1]}, ds2);
+            const float Dq = swap_halves_sum(ds2[0] + ds2[1]);
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+            for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int s_ = 0; s_ < 2; ++s_) frag_perm(buf, qb, s_, lo[qb][s_], hi[qb][s_]);
-        lds_wait();
+                for (int x2 = 0; x2 < 2; ++x2) {
+                    u32x4 du;
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+                    for (int e = 0; e < 8; e += 2) {
+                        const int x = 8 * x2 + e;
+                        const f32x2 p2 = unpk2<T>(__builtin_bit_cast(u32x4, pf[qb][kb][x2])[e >> 1]);
+                        const f32x2 t = (p2 * ((f32x2){acc[kb][qb][x], acc[kb][qb][x + 1]} - Dq)) * scale;
+                        du[e >> 1] = qv[qb] ? pk2<T>(t) : 0u;   // (select: dPᵀ of a query outside the window may be inf)
+                    }
+                    dsf[qb][kb][x2] = __builtin_bit_cast(F8, du);
+                }
+        }
+
+        // ---- phase B: dVᵀ = dOᵀ P, dKᵀ = Qᵀ (τ dS), dQᵀ = Kᵀ (τ dS)ᵀ, 32 output features at a time,
+        //      each stored through the 16-feature image in two passes ----
+        const int xs0 = cur.wx0 * st - g.pad, X0 = xs0 & ~7;   // strip start, its 16-B aligned base
+        const int xlo = max(xs0, 0), xhi = min(xs0 + cur.nvalid * ws, W_);
+        unsigned cm[4];                                  // slot-column mask of a 16-B row fragment
 #pragma unroll
-            for (int s_ = 0; s_ < 2; ++s_) {
-                lds_fence(lo[qb][s_]);
-                lds_fence(hi[qb][s_]);
-                const u32x4 u = {lo[qb][s_][0] & cm[2 * h], lo[qb][s_][1] & cm[2 * h + 1], hi[qb][s_][0] & cm[2 * h],
-                                 hi[qb][s_][1] & cm[2 * h + 1]};
-                const F8 a = __builtin_bit_cast(F8, u);
+        for (int j = 0; j < 4; ++j)
+            cm[j] = ((2 * j >= c0 && 2 * j < c1) ? 0x0000FFFFu : 0u) | ((2 * j + 1 >= c0 && 2 * j + 1 < c1) ? 0xFFFF0000u : 0u);
+        const StripStore sp = strip_store_plan(tid, y0, ws, H_, W_, X0, xlo, xhi);
+        // one 32 x 32 output block pair (features on accumulator rows, slot kb/qb * 32 + r on the
+        // lane) through the image: features 0..15, then 16..31
+        auto out_chunk = [&](const f32x16 (&oa)[2], T* base, int C, int fbase) __attribute__((always_inline)) {
+            const auto ors = slab_rsrc(base + (int64_t)b * C * P_, (uint32_t)(C * P_ * 2));
 #pragma unroll
-                for (int kb = 0; kb < 2; ++kb) oa[kb] = mfma32x32x16(a, xt[kb][qb][s_], oa[kb]);
+            for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    const int s = blk * 32 + r;
+                    if (slot_ok(s) && !(FA_WIN_ABL & 64)) {
+                        const uint32_t a0 = lds_off(img) + simg_pos(4 * h, s >> 3, ax + (s & 7) - X0);
+                        if (pass == 0) img_w8<T, 0>(a0, oa[blk]);
+                        else img_w8<T, 8>(a0, oa[blk]);
+                    }
+                }
+                lds_barrier();
+                strip_store16<T, PARTIAL>(img, ors, sp, tid, fbase + 16 * pass, C, P_);
+                if (!PARTIAL && !(FA_WIN_ABL & 32)) vm_issued += 2;
+                lds_barrier();                           // the image is free again
             }
-        lds_barrier();
+        };
+        // transpose: block (kb, qb) of X (B fragments, queries on lanes) -> keys on lanes, then
+        // B fragments [key block][query block][s'] whose query order is 16 s' + 4h + {0..3, 8..11}
+        auto transpose = [&](const F8 (&xf)[2][2][2], F8 (&xt)[2][2][2]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) img_write(buf, oa[kb], isk ? scale : 1.0f, kb * 32 + r);
-        lds_barrier();
-        if (isk) strip_store<T>(buf, dks, tid, c * 32, d, y0, ws, H_, W_, P_, X0, xlo, xhi);
-        else strip_store<T>(buf, dvs, tid, (c - NBQ) * 32, dv, y0, ws, H_, W_, P_, X0, xlo, xhi);
-        step_end(j);
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) {
+                    f32x16 c;
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) c[x] = 0.0f;
+                    c = mfma32x32x16(xf[qb][kb][0], id0, c);
+                    c = mfma32x32x16(xf[qb][kb][1], id1, c);
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) xt[kb][qb][x >> 3][x & 7] = (T)c[x];
+                }
+        };
+        // keys on lanes: oa[kb] = Σ A(f, queries) · xt[kb]
+        auto keys_out = [&](const u32x2 (&lo)[2][2], const u32x2 (&hi)[2][2], const F8 (&xt)[2][2][2], f32x16 (&oa)[2])
+            __attribute__((always_inline)) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) oa[kb][x] = 0.0f;
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int s_ = 0; s_ < 2; ++s_) {
+                    const u32x4 u = {lo[qb][s_][0] & cm[2 * h], lo[qb][s_][1] & cm[2 * h + 1], hi[qb][s_][0] & cm[2 * h],
+                                     hi[qb][s_][1] & cm[2 * h + 1]};
+                    const F8 af = __builtin_bit_cast(F8, u);
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb) oa[kb] = mfma32x32x16(af, xt[kb][qb][s_], oa[kb]);
+                }
+        };
+        F8 xt[2][2][2];
+        transpose(pf, xt);
+        // dVᵀ: dO rows from the (dO, V) images still in the ring; each frees two ring slots
+#pragma unroll
+        for (int c = 0; c < NCV; ++c) {
+            u32x2 lo[2][2], hi[2][2];
+            {
+                const int j = NQK + 2 * c + (r >> 4);    // this lane's feature's (dO, V) load
+                const char* buf = smem + slot_of(j) * BUF;
+                const int fl = r & 15;
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                    for (int s_ = 0; s_ < 2; ++s_) {
+                        lo[qb][s_] = lds_b64(buf + sqk_pos(fl, qb * 4 + 2 * s_, wl) + 8 * h);
+                        hi[qb][s_] = lds_b64(buf + sqk_pos(fl, qb * 4 + 2 * s_ + 1, wl) + 8 * h);
+                    }
+                lds_wait();
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                    for (int s_ = 0; s_ < 2; ++s_) { lds_fence(lo[qb][s_]); lds_fence(hi[qb][s_]); }
+            }
+            lds_barrier();                               // every wave has read both slots
+            refill(NQK + 2 * c);
+            refill(NQK + 2 * c + 1);
+            f32x16 oa[2];
+            keys_out(lo, hi, xt, oa);
+            out_chunk(oa, dvo, dv, 32 * c);
+            FA_BSTAMP(9 + c);
+        }
+        // dKᵀ (keys on lanes), from the Q stash
+        transpose(dsf, xt);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            f32x16 oa[2];
+            keys_out(qlo[c], qhi[c], xt, oa);
+            out_chunk(oa, dk, d, 32 * c);
+            FA_BSTAMP(11 + c);
+        }
+        // dQᵀ (queries on lanes), from the K stash
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            f32x16 oa[2];
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) oa[qb][x] = 0.0f;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    u32x4 kr = kst[c][kb][s2];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) kr[i] &= cm[i];
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb)
+                        oa[qb] = mfma32x32x16(__builtin_bit_cast(F8, kr), dsf[qb][kb][s2], oa[qb]);
+                }
+            out_chunk(oa, dq, d, 32 * c);
+            FA_BSTAMP(13 + c);
+        }
+        FA_BSTAMP(15);
+        cur = nxt;
+        gbase = (gbase + NA) & (R - 1);
     }
-    FA_STAMP(5);
 }
 
 // --------------------------------------------------------------------------
@@ -3120,16 +3334,28 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
     if (bwd_strip_ok(a)) {
         const int k0 = strip_first(a.g);
         const int64_t nsx = strip_count(a.g, k0), nstrip = nsx * a.g.O[1] * a.batch;
-#define FA_BWD_STRIP(DD, DVV)                                                                                   \
-    hipLaunchKernelGGL((win_bwd_strip<T, DD, DVV>), dim3((unsigned)nstrip), dim3(512), 0, s, (const T*)a.q,    \
+        // persistent: one workgroup per CU, equal rounds of strips (no partial last round)
+        const int64_t cus = device_cus(s) > 0 ? device_cus(s) : 256;
+        const int64_t rounds = (nstrip + cus - 1) / cus, grid = (nstrip + rounds - 1) / rounds;
+        // strip ends on 16-B chunks: every strip boundary (k0 aligns them) and the covered right end
+        const int64_t xend = a.g.O[0] * a.g.ws - a.g.pad;
+        const bool aligned = ((k0 * a.g.ws - a.g.pad) % 8 + 8) % 8 == 0 && (xend >= a.g.S[0] || xend % 8 == 0);
+#define FA_BWD_STRIP2(DD, DVV, PA)                                                                              \
+    hipLaunchKernelGGL((win_bwd_strip<T, DD, DVV, PA>), dim3((unsigned)grid), dim3(512), 0, s, (const T*)a.q,  \
                        (const T*)a.k, (const T*)a.v, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk, (T*)a.dv_, g, \
-                       (int)a.d, (int)a.dv, (int)nsx, k0, (int)nstrip, a.scale, a.scale * kLog2e)
+                       (int)a.d, (int)a.dv, (int)nsx, k0, (int)nstrip, (int)rounds, a.scale, a.scale * kLog2e)
+#define FA_BWD_STRIP(DD, DVV)                           \
+    do {                                                \
+        if (aligned) FA_BWD_STRIP2(DD, DVV, false);     \
+        else FA_BWD_STRIP2(DD, DVV, true);              \
+    } while (0)
         const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
         if (Dc == 32 && DVc == 32) FA_BWD_STRIP(32, 32);
         else if (Dc == 32) FA_BWD_STRIP(32, 64);
         else if (DVc == 32) FA_BWD_STRIP(64, 32);
         else FA_BWD_STRIP(64, 64);
 #undef FA_BWD_STRIP
+#undef FA_BWD_STRIP2
         if ((e = hipGetLastError()) != hipSuccess) {
             *why = hipGetErrorString(e);
             return FA_ERR_HIP;

@@ -1,16 +1,18 @@
 // Phase timestamps of the strip windowed backward (win_bwd_strip) at configs[2]
 // geometry: the product source included with FA_STAMP defined.  Phases:
-// 0 entry, 1 first load landed, 2 phase A (dPᵀ, Sᵀ) done, 3 P / D / dS done,
-// 4 dQ stored, 5 end (dK, dV stored).  Diagnostic only (never shipped);
+// 0 strip start, 1 + j load j landed (after its wait and barrier), 9..14 the six
+// gradient chunks (dV 0/1, dK 0/1, dQ 0/1) stored, 15 end,
+// per strip (the kernel is persistent: fa_sid
+// is the strip).  Diagnostic only (never shipped);
 // build / run: tools/exp/bwd_strip_stamp.py.
 #include <hip/hip_runtime.h>
-__device__ unsigned long long g_stamp_buf[8 * 16384];
-#define FA_STAMP(k)                                                                        \
+__device__ unsigned long long g_stamp_buf[24 * 16384];
+#define FA_BSTAMP(k)                                                                        \
     do {                                                                                   \
         if (threadIdx.x == 0) {                                                            \
-            ::g_stamp_buf[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime();            \
-            if ((k) == 0) ::g_stamp_buf[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime(); \
-            if ((k) == 5) ::g_stamp_buf[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime(); \
+            ::g_stamp_buf[fa_sid * 24 + (k)] = __builtin_amdgcn_s_memtime();            \
+            if ((k) == 0) ::g_stamp_buf[fa_sid * 24 + 16] = __builtin_amdgcn_s_memrealtime(); \
+            if ((k) == 15) ::g_stamp_buf[fa_sid * 24 + 17] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                                  \
     } while (0)
 #include "../../flashattention.jl_amd/csrc/fa_windowed.hip"
@@ -32,6 +34,6 @@ extern "C" int bwd_stamp_run(const void* q, const void* k, const void* v, const 
     if (rc != 0) return 1;
     if (!host_out) return 0;
     if (hipDeviceSynchronize() != hipSuccess) return 2;
-    if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamp_buf), sizeof(unsigned long long) * 8 * nwg_max) != hipSuccess) return 3;
+    if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamp_buf), sizeof(unsigned long long) * 24 * nwg_max) != hipSuccess) return 3;
     return 0;
 }

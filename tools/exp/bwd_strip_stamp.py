@@ -25,7 +25,7 @@ q, k, v, dy = (fa_hip.jl_tensor(torch.randn((128, 128, 64, Bimg), generator=g, d
 y, l, m = fa_hip.windowed_fa(q, k, v, 7)
 dq, dk, dv = (torch.empty_like(q) for _ in range(3))
 nwg = 3 * 19 * Bimg
-out = np.zeros(8 * nwg, dtype=np.uint64)
+out = np.zeros(24 * nwg, dtype=np.uint64)
 P = lambda t: ctypes.c_void_p(t.data_ptr())
 L.bwd_stamp_run.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
 args = (P(q), P(k), P(v), P(y), P(dy), P(l), P(m), P(dq), P(dk), P(dv), Bimg, 10)
@@ -43,14 +43,25 @@ for rep in range(3):
     us = e0.elapsed_time(e1) / 10 * 1e3
     rc = L.bwd_stamp_run(*args, out.ctypes.data_as(ctypes.c_void_p), nwg)
     assert rc == 0, rc
-    s = out.reshape(-1, 8).astype(np.int64)[:nwg]
-    ph = np.diff(s[:, :6], axis=1)
-    rt0, rt1 = s[:, 6], s[:, 7]
-    clk = (s[:, 5] - s[:, 0]) / np.maximum(rt1 - rt0, 1) * 100.0
-    names = ["first load", "phase A", "P/D/dS", "dQ", "dK + dV"]
-    print(f"abl {ABL} rep {rep}: {us:.1f} us/call; per-WG phase cycles (median / p90): " +
-          ", ".join(f"{n}: {np.median(ph[:, i]):.0f}/{np.percentile(ph[:, i], 90):.0f}" for i, n in enumerate(names)))
+    s = out.reshape(-1, 24).astype(np.int64)[:nwg]
+    st = s[:, :16]                                 # start, loads 0..7 landed, dV 0/1, dK 0/1, dQ 0/1 stored, end
+    ph = np.diff(st, axis=1)
+    rt0, rt1 = s[:, 16], s[:, 17]
+    clk = (s[:, 15] - s[:, 0]) / np.maximum(rt1 - rt0, 1) * 100.0
+    names = [f"->L{j}" for j in range(8)] + ["->dV0", "->dV1", "->dK0", "->dK1", "->dQ0", "->dQ1", "->end"]
+    print(f"abl {ABL} rep {rep}: {us:.1f} us/call; cycles between stamps (median / p90):")
+    print("   " + ", ".join(f"{n}: {np.median(ph[:, i]):.0f}/{np.percentile(ph[:, i], 90):.0f}" for i, n in enumerate(names)))
+    print(f"   WG total cycles median {np.median(s[:, 15] - s[:, 0]):.0f}, clock {np.median(clk):.0f} MHz; WG span median "
+          f"{np.median(rt1 - rt0) / 100:.2f} us", flush=True)
     span = rt1.max() - rt0.min()
-    print(f"   WG total cycles median {np.median(s[:, 5] - s[:, 0]):.0f}, clock {np.median(clk):.0f} MHz; WG span median "
-          f"{np.median(rt1 - rt0) / 100:.2f} us; kernel span {span / 100:.1f} us; WGs in flight (sum of spans / span) "
-          f"{(rt1 - rt0).sum() / span:.0f}", flush=True)
+    print(f"   kernel span {span / 100:.1f} us; strips in flight (sum of spans / span) {(rt1 - rt0).sum() / span:.0f}",
+          flush=True)
+    per = (nwg + 255) // 256                       # the launcher's persistent plan (256 CUs): consecutive strips
+    G = (nwg + per - 1) // per
+    sl = [slice(i * per, min((i + 1) * per, nwg)) for i in range(G)]
+    wg0 = np.array([rt0[x].min() for x in sl]); wg1 = np.array([rt1[x].max() for x in sl])
+    busy = np.array([(rt1[x] - rt0[x]).sum() for x in sl])
+    t0m = rt0.min()
+    print(f"   {G} WGs: start (us after first) median {np.median(wg0 - t0m) / 100:.1f} max {(wg0 - t0m).max() / 100:.1f}; "
+          f"end median {np.median(wg1 - t0m) / 100:.1f} p10 {np.percentile(wg1 - t0m, 10) / 100:.1f} max {(wg1 - t0m).max() / 100:.1f}; "
+          f"busy/lifetime median {np.median(busy / (wg1 - wg0)):.3f}", flush=True)
