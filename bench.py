@@ -329,7 +329,7 @@ def cfg2_block(fa, dist, steps=20):
     (+ l, m) for the backward (y is not needed: the strip backward forms
     D = rowsum(P ∘ dP); the one-window kernel still reads it); GB/s against 8 TB/s.
     Kernels: B = 1 runs the per-window kernels, B = 32 the strip kernels
-    (>= 512 / 256 strips)."""
+    (>= 256 strips)."""
     gen = torch.Generator(device="cuda").manual_seed(11)
     T, L, S, dd = 49, 19 * 19, 128 * 128, 64
     res = {"workload": "configs[2]: windowed_fa 2-D bf16, 128x128 image, ws=7, d=64, stride 7, pad 3",
@@ -344,7 +344,7 @@ def cfg2_block(fa, dist, steps=20):
         res[f"B{Bimg}"] = {
             "fwd_us": t * 1e6, "fwd_GBs": by / t / 1e9, "fwd_frac_hbm": by / t / 1e9 / PEAK_HBM_GBS,
             "fwd_bytes": by,
-            "fwd_kernel": "fa::win_strip<bf16,64,64>" if Bimg >= 9 else "fa::win_rows1s<bf16,64,64,2>",
+            "fwd_kernel": "fa::win_strip<bf16,64,64>" if Bimg >= 5 else "fa::win_rows1s<bf16,64,64,2>",
             "bwd_us": tb * 1e6, "bwd_GBs": bb / tb / 1e9, "bwd_frac_hbm": bb / tb / 1e9 / PEAK_HBM_GBS,
             "bwd_bytes": bb,
             "bwd_kernel": "fa::win_bwd_strip<bf16,64,64>" if Bimg >= 5 else "fa::win_bwd_rows<bf16,64,64>"}

@@ -1248,7 +1248,9 @@ __global__ __launch_bounds__(256 * NW, 8) void win_dma(const T* __restrict__ q, 
 // the softmax analytically (npad zero keys), padding rows load as zeros.
 // LDS-DMA writes lane-linearly, so the swizzles are applied through each lane's
 // choice of (window, slot row):
-//   Q / K: window position w ^ ((f & 3) | ((c >> 1) & 1) << 2)  (ds_read_b64_tr_b16, conflict-free);
+//   Q / K: window position w ^ (f & 7) ^ ((c >> 1) & 1) << 2  (ds_read_b64_tr_b16: f & 4 is fixed per
+//          instruction, so this is the conflict-free (f & 3, c) pattern; the 16-B row reads of the
+//          strip backward's register stash, 16 features at a time, then meet 2-way conflicts, not 4);
 //   V    : slot-row position c ^ ((f >> 3) & 1), window position w ^ (f & 7)  (ds_read_b128, conflict-free).
 // --------------------------------------------------------------------------
 constexpr int kStripW = 8;                          // windows per strip workgroup
@@ -1272,8 +1274,9 @@ __device__ __forceinline__ int simg_swz(int f, int row) { return ((row >> 1) & 3
 __device__ __forceinline__ int simg_pos(int f, int row, int px) {
     return f * 1024 + row * 128 + (((px >> 3) ^ simg_swz(f, row)) << 4) + (px & 7) * 2;
 }
+__device__ __forceinline__ int sqk_swz(int f, int c) { return (f & 7) ^ (((c >> 1) & 1) << 2); }
 __device__ __forceinline__ int sqk_pos(int f, int c, int w) {   // byte offset in a Q / K chunk image
-    return f * 1024 + c * 128 + ((w ^ ((f & 3) | (((c >> 1) & 1) << 2))) << 4);
+    return f * 1024 + c * 128 + ((w ^ sqk_swz(f, c)) << 4);
 }
 __device__ __forceinline__ int sv_pos(int f, int c, int w) {    // byte offset in a V chunk image
     return f * 1024 + ((c ^ ((f >> 3) & 1)) << 7) + ((w ^ (f & 7)) << 4);
@@ -1313,7 +1316,7 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
     // hipcc's host pass drop the kernel's launch stub, with no diagnostic)
     auto dma_qk = [&](__amdgpu_buffer_rsrc_t rs, char* img, int fl, int fg) {
         const int pc = lane >> 3, pw = lane & 7;
-        const int w = pw ^ ((fl & 3) | (((pc >> 1) & 1) << 2)), y = y0 + pc;
+        const int w = pw ^ sqk_swz(fl, pc), y = y0 + pc;
         const bool ok = w < nvalid && pc < ws && y >= 0 && y < H_ && fg < d;
         const int off = ok ? (fg * P_ + y * W_ + ax_of(w)) * 2 : 0x7FFFFFF0;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + fl * 1024), 16,
@@ -1378,10 +1381,10 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
         for (int blk = 0; blk < 2; ++blk) {
             const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
             rk[blk][0] = lds_tr16(a);
-            rk[blk][1] = lds_tr16(a + 4 * 1024);
+            rk[blk][1] = lds_tr16(buf + 16384 + sqk_pos(8 * h + qq + 4, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8);
             const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
             rq[blk][0] = lds_tr16(aq);
-            rq[blk][1] = lds_tr16(aq + 4 * 1024);
+            rq[blk][1] = lds_tr16(buf + sqk_pos(8 * h + qq + 4, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8);
         }
         lds_wait();
         F8 kf[2], qf[2];
@@ -2153,7 +2156,7 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
     auto dma_qk = [&](const StripPos& p, __amdgpu_buffer_rsrc_t rs, char* im, int fl, int fg, int C)
         __attribute__((always_inline)) {
         const int pc = lane >> 3, pw = lane & 7;
-        const int w = pw ^ ((fl & 3) | (((pc >> 1) & 1) << 2)), y = p.y0 + pc;
+        const int w = pw ^ sqk_swz(fl, pc), y = p.y0 + pc;
         const bool ok = w < p.nvalid && pc < ws && y >= 0 && y < H_ && fg < C;
         const int off = ok ? (fg * P_ + y * W_ + ax_of(p, w)) * 2 : 0x7FFFFFF0;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(im + fl * 1024), 16,
@@ -2318,10 +2321,10 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
             for (int blk = 0; blk < 2; ++blk) {
                 const char* a = buf + 16384 + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8;
                 rk[blk][0] = lds_tr16(a);
-                rk[blk][1] = lds_tr16(a + 4 * 1024);
+                rk[blk][1] = lds_tr16(buf + 16384 + sqk_pos(8 * h + qq + 4, 4 * blk + 2 * kh + (sig >> 1), wl) + (sig & 1) * 8);
                 const char* aq = buf + sqk_pos(8 * h + qq, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8;
                 rq[blk][0] = lds_tr16(aq);
-                rq[blk][1] = lds_tr16(aq + 4 * 1024);
+                rq[blk][1] = lds_tr16(buf + sqk_pos(8 * h + qq + 4, 4 * blk + 2 * kh + (pp >> 1), wl) + (pp & 1) * 8);
             }
             if (j < NQK) {                               // this chunk's 16 features of the K / Q stashes
                 const int c = j >> 1, fl = r & 15;
@@ -2509,8 +2512,10 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
                     for (int kb = 0; kb < 2; ++kb) oa[kb] = mfma32x32x16(af, xt[kb][qb][s_], oa[kb]);
                 }
         };
+        FA_BSTAMP(18);
         F8 xt[2][2][2];
         transpose(pf, xt);
+        FA_BSTAMP(19);
         // dVᵀ: dO rows from the (dO, V) images still in the ring; each frees two ring slots
 #pragma unroll
         for (int c = 0; c < NCV; ++c) {
@@ -2533,10 +2538,12 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
                     for (int s_ = 0; s_ < 2; ++s_) { lds_fence(lo[qb][s_]); lds_fence(hi[qb][s_]); }
             }
             lds_barrier();                               // every wave has read both slots
-            refill(NQK + 2 * c);
-            refill(NQK + 2 * c + 1);
+            if (c == 0) FA_BSTAMP(20);
             f32x16 oa[2];
             keys_out(lo, hi, xt, oa);
+            refill(NQK + 2 * c);
+            refill(NQK + 2 * c + 1);
+            if (c == 0) FA_BSTAMP(21);
             out_chunk(oa, dvo, dv, 32 * c);
             FA_BSTAMP(9 + c);
         }
@@ -2942,7 +2949,7 @@ static int rows_kind(const WindowedArgs& a) {
 // Strip kernel (win_strip) from this many workgroups on: below it the eight-window
 // workgroups leave CUs idle and the two-window kernel's latency wins (configs[2] at
 // B = 1 is 57 strips).
-constexpr int64_t kStripMin = 512;
+constexpr int64_t kStripMin = 256;
 
 // Windows of the first strip: the smallest k0 in 1..8 with k0 * ws = pad (mod 8),
 // so that every later strip starts on a 16-B chunk of y (8 otherwise).

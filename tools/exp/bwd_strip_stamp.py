@@ -51,6 +51,10 @@ for rep in range(3):
     names = [f"->L{j}" for j in range(8)] + ["->dV0", "->dV1", "->dK0", "->dK1", "->dQ0", "->dQ1", "->end"]
     print(f"abl {ABL} rep {rep}: {us:.1f} us/call; cycles between stamps (median / p90):")
     print("   " + ", ".join(f"{n}: {np.median(ph[:, i]):.0f}/{np.percentile(ph[:, i], 90):.0f}" for i, n in enumerate(names)))
+    sub = np.stack([s[:, 8], s[:, 18], s[:, 19], s[:, 20], s[:, 21], s[:, 9]], axis=1)
+    sd = np.diff(sub, axis=1)
+    print("   within L7->dV0: " + ", ".join(f"{n}: {np.median(sd[:, i]):.0f}/{np.percentile(sd[:, i], 90):.0f}" for i, n in
+          enumerate(["D, dS", "Pᵀ transpose", "dO reads", "dV MFMA + refill", "dV image + stores"])))
     print(f"   WG total cycles median {np.median(s[:, 15] - s[:, 0]):.0f}, clock {np.median(clk):.0f} MHz; WG span median "
           f"{np.median(rt1 - rt0) / 100:.2f} us", flush=True)
     span = rt1.max() - rt0.min()
