@@ -131,12 +131,12 @@ int fa_debug_set_bwd_generic(int v) {
 // hand-off's timeout word preset, which exercises the dQ fallback pass).  Builds with
 // -DFA_BWD_ABL also accept the timing-only ablations of the single pass, which compute
 // a WRONG dQ: 4, 5, 6 no waits, no running-sum traffic, neither; 7, 8 no running-sum
-// loads / stores; 9 no dS image writes.  Any other value is rejected (returns -1, the
+// loads / stores; 9 no dS image writes; 10 no next-slice Q/dO DMA; 11 = 10 + 6.  Any other value is rejected (returns -1, the
 // mode is unchanged).
 int fa_debug_set_bwd_mode(int v) {
     const int old = fa::g_bwd_mode;
 #ifdef FA_BWD_ABL
-    constexpr int kMaxMode = 9;
+    constexpr int kMaxMode = 11;
 #else
     constexpr int kMaxMode = 3;
 #endif

@@ -19,6 +19,7 @@
 // N % 8 == 0) and a generic LDS-tiled SIMT path (fp32, ragged or unaligned
 // shapes) used for parity on every dtype.
 #include <type_traits>
+#include <utility>
 
 #include "fa_common.h"
 #include "fa_internal.h"
@@ -888,6 +889,44 @@ __device__ __noinline__ void wait_count(gu32* f, unsigned want, gu32* err) {
     }
 }
 
+// LDS reads hidden from the compiler, with an immediate offset.  hipcc makes every
+// LDS access it can see after a `buffer_load ... lds` wait for ALL outstanding
+// vector-memory operations (s_waitcnt vmcnt(0): it cannot tell which buffer a DMA
+// writes), which in bwd_fused put the next slice's Q/dO DMA and the running-sum
+// loads in front of the dQ phase.  A result is not ready until an lgkmcnt wait;
+// pass it through reg_fence() after that wait, before any use.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_b128_at(uint32_t a) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+    return r;
+}
+template <int OFF>
+__device__ __forceinline__ s16x4 lds_tr16_at(uint32_t a) {
+    s16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+    return r;
+}
+__device__ __forceinline__ void lds_w32(void* p, float v) {
+    asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(p)), "v"(v) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(%0)" : : "i"(N) : "memory"); }
+template <class X>
+__device__ __forceinline__ void reg_fence(X& x) { asm volatile("" : "+v"(x)); }
+// A copy of x the compiler cannot see through: values derived from it inside a loop
+// are not hoisted (hoisted per-lane addresses stay live across the loop and spill).
+__device__ __forceinline__ int opaque(int x) { asm volatile("" : "+v"(x)); return x; }
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl(f, std::make_integer_sequence<int, N>{}); }
+
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     typedef typename Frag8<T>::type F8;
@@ -904,6 +943,11 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     float* const rowc = (float*)(oimg + OB);       // −lse[64] (raw units), −D[64]
     char* const dsimg = qimg + STAGE;
 
+#ifdef FA_BWD_ABL
+    const int abl = p.ablate;
+#else
+    constexpr int abl = 0;   // the timing-only ablations exist only in -DFA_BWD_ABL builds
+#endif
     const int lid = p.xcd ? xcd_remap(blockIdx.x, p.total_wg) : (int)blockIdx.x;
     const int KM = p.nkb, NS = p.nqt, OFF = p.hoff;   // members per slab, slices
     const int b = lid / KM, j = lid - b * KM;
@@ -945,11 +989,6 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     };
     auto rowfrag = [&](const char* img, int cb, int tb, int s2) -> F8 {
         return *(const F8*)(img + (cb * 32 + r) * 128 + (((tb * 4 + 2 * s2 + h) ^ rsw) * 16));
-    };
-    auto trat = [&](const char* a) -> F8 {   // transposed fragment at a per-lane address
-        const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
-        const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
-        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
     auto slice_of = [&](int i) {
         int t = (i - OFF * j) % NS;
@@ -1002,26 +1041,25 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const int ktb = wave & 1;
     const int dsrow = 32 * wave + sig32(r);                  // this lane's dSᵀ row
     const int cbq = wave % (D / 32), uq = wave / (D / 32);   // this wave's dQᵀ tile (wave < NTQ)
-    // transposed-read offset into the dSᵀ image (its own swizzle swzds; row 16 kk + 8h + qq)
-    const int trds = (8 * h + qq) * 128 + (((uq * 4 + kh * 2 + (sig >> 1)) ^ swzds(8 * h + qq)) * 16) + (sig & 1) * 8;
 
     int t_prev = 0, pos_prev = 0;
     bool pub_prev = false;
     for (int i = 0; i < NS; ++i) {
         t = slice_of(i);
         const int pos = chain_pos(t);
+        const int tq = opaque(tid), lq = tq & 63, rq = lq & 31, hq = lq >> 5;   // re-derived per step
         const bool tail = pos == KM - 1;
         // B1: this slice's images landed, last step's sums drained; one lane has
         // seen the predecessor's count for slice t (the barrier releases the rest)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (pos > 0 && tid == 0 && !(p.ablate & 1)) wait_count(flg + t, (unsigned)pos, err);
+        if (pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, err);
         __syncthreads();
         if (pub_prev && tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
-        const bool has_tile = wave < NTQ;
-        const int pofs = (t * NTQ + wave) * 4096 + lane * 16;
-        const bool ldpin = pos > 0 && has_tile && !(p.ablate & 10);
+        const bool has_tile = NTQ >= 8 || wave < NTQ;
+        const int pofs = (t * NTQ + wave) * 4096 + lq * 16;
+        const bool ldpin = pos > 0 && has_tile && !(abl & 10);
         u32x4 pin[4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -1056,25 +1094,32 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 for (int s2 = 0; s2 < 2; ++s2) dk[cb] = mfma32x32x16(rowfrag(qimg, cb, u, s2), dsf[s2], dk[cb]);
             // dSᵀ row kj: queries 32u + 16 s2 + 8h + {0..7}
 #pragma unroll
-            for (int s2 = 0; s2 < 2 && !(p.ablate & 32); ++s2)
+            for (int s2 = 0; s2 < 2 && !(abl & 32); ++s2)
                 *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow)) * 16)) = dsf[s2];
         }
 
-        // running sum of the members before this one (sc1 loads, after B1; issuing
-        // them halfway through this phase instead measured the same)
-        if (ldpin) {
+        // running sum of the members before this one (sc1 loads, after B1).  Loaded
+        // whether or not this member is the chain's head (which adds nothing), and the
+        // DMA and row constants below are unconditional too: a straight-line step
+        // lets the compiler count vmcnt for the sums past the DMA instead of vmcnt(0).
+        if (has_tile && !(abl & 10)) {
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) pin[c4] = __builtin_amdgcn_raw_buffer_load_b128(prs, pofs + c4 * 1024, 0, 16);
         }
         __syncthreads();   // B2: dSᵀ complete, the slice's images free
 
         // next slice's images and row constants (land before the next B1)
-        float rc = 0.0f;
-        if (i + 1 < NS) {
-            const int tn = slice_of(i + 1);
-            rc = load_rowc(tn);
-            dma_image8<D>(qrs, qimg, N, tn * 64, wave, lane);
-            dma_image8<DV>(ors, oimg, N, tn * 64, wave, lane);
+        // (the last step reloads its own slice: harmless, nothing reads it)
+        float rc;
+        {
+            const int tn = i + 1 < NS ? slice_of(i + 1) : t;
+            const int q = tn * 64 + lq;
+            const float v = (tq < 64 ? nlse : nDg)[q < N ? q : N - 1];
+            rc = q < N ? v : (tq < 64 ? kNegInf : 0.0f);
+            if (!(abl & 64)) {
+                dma_image8<D>(qrs, qimg, N, tn * 64, wave, lq);
+                dma_image8<DV>(ors, oimg, N, tn * 64, wave, lq);
+            }
         }
 
         // ---- dQᵀ tile (features 32 cbq.., queries 32 uq..) over the 256 keys ----
@@ -1082,10 +1127,42 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             f32x16 acc;
 #pragma unroll
             for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
+            // asm LDS reads (see lds_b128_at), one step ahead of the MFMA: the DMA
+            // just issued and the running-sum loads stay in flight meanwhile
+            uint32_t ka[4];
+            const int rswq = swz16(rq);
 #pragma unroll
-            for (int kk = 0; kk < 16; ++kk)
-                acc = mfma32x32x16(rowfrag(kimg + (kk >> 2) * KSUB, cbq, (kk >> 1) & 1, kk & 1),
-                                   trat(dsimg + trds + 16 * kk * 128), acc);
+            for (int q4 = 0; q4 < 4; ++q4)
+                ka[q4] = lds_addr(kimg + (cbq * 32 + rq) * 128 + ((((q4 >> 1) * 4 + 2 * (q4 & 1) + hq) ^ rswq) * 16));
+            const int qqq = (lq & 15) >> 2, ppq = lq & 3, khq = (lq >> 4) & 1;
+            const int sgq = (ppq == 1) ? 2 : (ppq == 2) ? 1 : ppq;
+            const uint32_t da = lds_addr(dsimg + (8 * hq + qqq) * 128 +
+                                         (((uq * 4 + khq * 2 + (sgq >> 1)) ^ swzds(8 * hq + qqq)) * 16) + (sgq & 1) * 8);
+            u32x4 fa[2];
+            s16x4 flo[2], fhi[2];
+            auto issue = [&](auto kc) {
+                constexpr int kk = decltype(kc)::value;
+                fa[kk & 1] = lds_b128_at<(kk >> 2) * KSUB>(ka[kk & 3]);
+                flo[kk & 1] = lds_tr16_at<2048 * kk>(da);
+                fhi[kk & 1] = lds_tr16_at<2048 * kk + 512>(da);
+            };
+            issue(std::integral_constant<int, 0>{});
+            static_for<16>([&](auto kc) {
+                constexpr int kk = decltype(kc)::value;
+                if constexpr (kk + 1 < 16) {
+                    issue(std::integral_constant<int, kk + 1>{});
+                    lgkm_wait<3>();
+                } else {
+                    lgkm_wait<0>();
+                }
+                reg_fence(fa[kk & 1]);
+                reg_fence(flo[kk & 1]);
+                reg_fence(fhi[kk & 1]);
+                const F4 lo = __builtin_bit_cast(F4, flo[kk & 1]);
+                const F4 hi = __builtin_bit_cast(F4, fhi[kk & 1]);
+                acc = mfma32x32x16(__builtin_bit_cast(F8, fa[kk & 1]), __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                   acc);
+            });
             if (ldpin) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4)
@@ -1094,14 +1171,14 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             }
             if (tail) {
                 // 32-bit lane offset + scalar row offset (no hoisted 64-bit addresses)
-                const int q = t * 64 + 32 * uq + sig32(r);
+                const int q = t * 64 + 32 * uq + sig32(rq);
                 const auto qo = bslab<T>(p.dQ, (int64_t)b * N * D, (int64_t)N * D);
-                const int vo = q < N ? ((cbq * 32 + 4 * h) * N + q) * 2 : N * D * 2;   // past N: dropped
+                const int vo = q < N ? ((cbq * 32 + 4 * hq) * N + q) * 2 : N * D * 2;   // past N: dropped
 #pragma unroll
                 for (int x = 0; x < 16; ++x)
                     __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[x] * p.scale)), qo, vo,
                                                           ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
-            } else if (!(p.ablate & 18)) {
+            } else if (!(abl & 18)) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4) {
                     const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
@@ -1110,7 +1187,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 }
             }
         }
-        if (i + 1 < NS && tid < 128) rowc[tid] = rc;
+        if (i + 1 < NS && tq < 128) lds_w32(rowc + tq, rc);   // asm: no vmcnt(0) on the DMA
         t_prev = t;
         pos_prev = pos;
         pub_prev = !tail;
@@ -1362,7 +1439,8 @@ static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStr
     // guarded dQ pass must recompute dQ
     p.hdr_err = g_bwd_mode == 3 ? 1u : 0u;
 #ifdef FA_BWD_ABL
-    p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
+    p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode == 10 ? 64
+             : g_bwd_mode == 11 ? 64 | 3 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
 #endif
     return hipMemsetAsync(w, 0, fz.flag_bytes, s);
 }
