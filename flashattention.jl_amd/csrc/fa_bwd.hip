@@ -876,7 +876,7 @@ __device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img,
 constexpr uint64_t kSpinTicks = 2000000;   // s_memrealtime (100 MHz): 20 ms
 
 // One lane waits until *f >= want; false after a timeout (then *err = 1).
-__device__ __noinline__ void wait_count(gu32* f, unsigned want, gu32* err) {
+__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* err) {
     if (ld_agent(f) >= want) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -927,6 +927,49 @@ __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int
 template <int N, class F>
 __device__ __forceinline__ void static_for(F&& f) { static_for_impl(f, std::make_integer_sequence<int, N>{}); }
 
+// Buffer descriptor as four SGPRs for inline asm (raw buffer, stride 0, the
+// make_buffer_rsrc flags used everywhere here).
+__device__ __forceinline__ u32x4 desc_of(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    return u32x4{(unsigned)a, (unsigned)(a >> 32), bytes, 0x00020000u};
+}
+// Vector-memory operations hidden from the compiler's waitcnt model: the caller
+// counts vmcnt for them (they retire in issue order) and fences the results.
+__device__ __forceinline__ void dma16_asm(const u32x4& desc, uint32_t lds_base, int voff) {
+    asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ u32x4 load16_sc1_asm(const u32x4& desc, int voff) {
+    u32x4 r;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 sc1" : "=v"(r) : "v"(voff), "s"(desc), "i"(OFF) : "memory");
+    return r;
+}
+// dma_image8 through dma16_asm; returns nothing, issues (R/8 + 7)/8 ops or fewer per wave
+template <int R>
+__device__ __forceinline__ void dma_image8_asm(const u32x4& desc, char* img, int ntok, int t0, int wave, int lane) {
+    constexpr int NB = R / 8;
+#pragma unroll
+    for (int it = 0; it < (NB + 7) / 8; ++it) {
+        const int blk = it * 8 + wave;
+        if (NB % 8 == 0 || blk < NB) {
+            const int P = blk * 64 + lane;
+            const int f = P >> 3, c = (P & 7) ^ swz16(f);
+            dma16_asm(desc, lds_addr(img + blk * 1024), (f * ntok + t0 + 8 * c) * 2);
+        }
+    }
+}
+__device__ __forceinline__ float load4_asm(const float* p) {
+    float r;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+// vmcnt immediates (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4] = 7, lgkmcnt[11:8] = 15)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 16, "vmcnt");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+}
+
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     typedef typename Frag8<T>::type F8;
@@ -967,6 +1010,11 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const int64_t pslab = (int64_t)NS * NTQ * 1024;   // floats of running sums per slab
     const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.part + b * pslab), (short)0, (int)(pslab * 4),
                                                        0x00020000);
+    const u32x4 pdesc = desc_of(p.part + b * pslab, (uint32_t)(pslab * 4));
+    const u32x4 qdesc = desc_of((const T*)p.Q + (int64_t)b * N * D, (uint32_t)(N * D * 2));
+    const u32x4 odesc = desc_of((const T*)p.dO + (int64_t)b * N * DV, (uint32_t)(N * DV * 2));
+    // this wave's loop DMA ops per slice (dma_image8_asm), >= for every wave: a lower bound
+    constexpr int NDMA = (D / 8 >= 8 ? D / 64 : 0) + (DV / 8 >= 8 ? DV / 64 : 0);
     gu32* const flg = (gu32*)(p.flags + (int64_t)b * NS);
     gu32* const err = (gu32*)p.err;
 
@@ -1044,20 +1092,28 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 
     int t_prev = 0, pos_prev = 0;
     bool pub_prev = false;
+    // the prologue's loads have landed: no LDS-DMA the compiler knows of is pending in
+    // the loop (its DMA is asm), so it adds no vmcnt(0) before the loop's LDS reads
+    vm_wait<0>();
     for (int i = 0; i < NS; ++i) {
         t = slice_of(i);
         const int pos = chain_pos(t);
         const int tq = opaque(tid), lq = tq & 63, rq = lq & 31, hq = lq >> 5;   // re-derived per step
         const bool tail = pos == KM - 1;
-        // B1: this slice's images landed, last step's sums drained; one lane has
-        // seen the predecessor's count for slice t (the barrier releases the rest)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, err);
+        // B1: this slice's images landed; lane 0 has seen the predecessor's count for
+        // slice t (polled at the end of the previous step's dQ phase, or here for the
+        // first step; the barrier releases the other waves' sum loads).  The previous
+        // step's running-sum stores (this wave's last >= 4 vector-memory ops) may still
+        // be in flight: every wave drains them in the middle of phase A and their count
+        // is published after B2.  (vmcnt retires in issue order; a poll load behind
+        // those stores would wait for them, hence the poll's place.)
+        const bool has_tile = NTQ >= 8 || wave < NTQ;
+        if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
+        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, err);
         __syncthreads();
-        if (pub_prev && tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
-        const bool has_tile = NTQ >= 8 || wave < NTQ;
         const int pofs = (t * NTQ + wave) * 4096 + lq * 16;
         const bool ldpin = pos > 0 && has_tile && !(abl & 10);
         u32x4 pin[4];
@@ -1077,6 +1133,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             for (int s = 0; s < D / 16; ++s) sa = mfma32x32x16(trfrag(qimg, u, s), trfrag(kmine, ktb, s), sa);
 #pragma unroll
             for (int s = 0; s < DV / 16; ++s) dp = mfma32x32x16(trfrag(oimg, u, s), vf[s], dp);
+            if (u == 1) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): last step's sums stored
             F8 pf[2], dsf[2];
 #pragma unroll
             for (int x = 0; x < 16; ++x) {
@@ -1102,23 +1159,34 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // whether or not this member is the chain's head (which adds nothing), and the
         // DMA and row constants below are unconditional too: a straight-line step
         // lets the compiler count vmcnt for the sums past the DMA instead of vmcnt(0).
-        if (has_tile && !(abl & 10)) {
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) pin[c4] = __builtin_amdgcn_raw_buffer_load_b128(prs, pofs + c4 * 1024, 0, 16);
+        // lane 0 polls for the NEXT step's slice here: every wave's queue is empty
+        // (drained in the middle of this phase), so the poll pays only its own latency,
+        // and barriers B2 and B1 order it before every wave's sum loads of that step
+        if (wave == 0 && i + 1 < NS && !(abl & 1)) {
+            const int tn = slice_of(i + 1), pn = chain_pos(tn);
+            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, err);
         }
-        __syncthreads();   // B2: dSᵀ complete, the slice's images free
+        if (has_tile && !(abl & 10)) {
+            pin[0] = load16_sc1_asm<0>(pdesc, pofs);
+            pin[1] = load16_sc1_asm<1024>(pdesc, pofs);
+            pin[2] = load16_sc1_asm<2048>(pdesc, pofs);
+            pin[3] = load16_sc1_asm<3072>(pdesc, pofs);
+        }
+        __syncthreads();   // B2: dSᵀ complete, the slice's images free, last step's sums stored
+        if (pub_prev && tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
 
         // next slice's images and row constants (land before the next B1)
         // (the last step reloads its own slice: harmless, nothing reads it)
         float rc;
+        bool rc_in;
         {
             const int tn = i + 1 < NS ? slice_of(i + 1) : t;
             const int q = tn * 64 + lq;
-            const float v = (tq < 64 ? nlse : nDg)[q < N ? q : N - 1];
-            rc = q < N ? v : (tq < 64 ? kNegInf : 0.0f);
+            rc = load4_asm((tq < 64 ? nlse : nDg) + (q < N ? q : N - 1));   // asm: counted below
+            rc_in = q < N;
             if (!(abl & 64)) {
-                dma_image8<D>(qrs, qimg, N, tn * 64, wave, lq);
-                dma_image8<DV>(ors, oimg, N, tn * 64, wave, lq);
+                dma_image8_asm<D>(qdesc, qimg, N, tn * 64, wave, lq);
+                dma_image8_asm<DV>(odesc, oimg, N, tn * 64, wave, lq);
             }
         }
 
@@ -1163,6 +1231,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 acc = mfma32x32x16(__builtin_bit_cast(F8, fa[kk & 1]), __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7),
                                    acc);
             });
+            // the sums (asm loads): all but this wave's NDMA DMA ops retired
+            if (!(abl & 64)) vm_wait<NDMA>(); else vm_wait<0>();
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) reg_fence(pin[c4]);
+            reg_fence(rc);
+            // the next slice's row constants (phase A's reads of rowc ended at B2)
+            if (tq < 128) lds_w32(rowc + tq, rc_in ? rc : (tq < 64 ? kNegInf : 0.0f));
             if (ldpin) {
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4)
@@ -1187,7 +1262,6 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 }
             }
         }
-        if (i + 1 < NS && tq < 128) lds_w32(rowc + tq, rc);   // asm: no vmcnt(0) on the DMA
         t_prev = t;
         pos_prev = pos;
         pub_prev = !tail;
