@@ -840,6 +840,13 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // through the workspace with sc1 stores, a per-slice counter (one lane, sc1) that the
 // next member polls (one lane) before a barrier, and sc1 loads
 // (MI355X_MICROARCH § visibility, first row of the sc1 hand-off table; 1 WG per CU).
+// Step i of a member, in issue order: B1 (vmcnt(4): slice i's Q/dO DMA landed, step
+// i-1's four sum stores may still fly) | phase A, u = 0 | vmcnt(0): step i-1's sums
+// stored | u = 1 | lane 0 polls the count of step i+1's slice; the sum loads of step i
+// | B2; lane 0 publishes step i-1's count | the row constants and Q/dO DMA of step
+// i+1 | the dQ tile (asm LDS reads) | vmcnt(NDMA): the sums landed, added | the sum
+// stores (or the tail's dQ stores).  So no barrier waits on a store, and the only
+// vmcnt(0) of a step is the one in the middle of phase A.
 // Every member of a slab must be resident at once: dispatch order within an XCD
 // is monotone, so a slab's members are dealt either to one XCD (K <= 32) or across
 // all of them; each poll is bounded (~20 ms of s_memrealtime), and a timeout sets
