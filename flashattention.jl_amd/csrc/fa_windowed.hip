@@ -768,6 +768,17 @@ __device__ __forceinline__ void lds_w16(void* p, unsigned v) {
     asm volatile("ds_write_b16 %0, %1" : : "v"(lds_off(p)), "v"(v) : "memory");
 }
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_w32u(void* p, unsigned v) {
+    asm volatile("ds_write_b32 %0, %1" : : "v"(lds_off(p)), "v"(v) : "memory");
+}
+// Returning agent-scope atomic add, hidden from the compiler's waitcnt model (the
+// caller counts it in its vmcnt bookkeeping and fences the result after the wait).
+__device__ __forceinline__ unsigned atomic_add_ret(unsigned* p, unsigned v) {
+    unsigned r;
+    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(v) : "memory");
+    return r;
+}
+
 template <class X>
 __device__ __forceinline__ void lds_fence(X& x) { asm volatile("" : "+v"(x)); }
 
@@ -2122,7 +2133,7 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
                                                         const float* __restrict__ lw, const float* __restrict__ mw,
                                                         T* __restrict__ dq, T* __restrict__ dk, T* __restrict__ dvo,
                                                         WinDev g, int d, int dv, int nsx, int k0, int nstrip,
-                                                        int per, float scale, float scale_log2) {
+                                                        unsigned* __restrict__ ctr, float scale, float scale_log2) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
     static_assert(D % 32 == 0 && D <= 64 && DV % 32 == 0 && DV <= 64, "head dims");
@@ -2130,9 +2141,10 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
     constexpr int NC = D / 32, NCV = DV / 32;        // 32-feature output chunks of dQ / dK and of dV
     constexpr int R = 4, BUF = 32768, IMG = 16384;
     static_assert(NA >= R, "every ring slot is a load of the strip");
-    __shared__ __attribute__((aligned(16))) char smem[R * BUF + IMG + 2 * 2 * 8 * 64 * 4];
+    __shared__ __attribute__((aligned(16))) char smem[R * BUF + IMG + 2 * 2 * 8 * 64 * 4 + 16];
     char* const img = smem + R * BUF;                // 16-feature gradient image
     float* const lms = (float*)(img + IMG);          // l, m of a strip's windows: [parity][l | m][window][64]
+    unsigned* const nsid_lds = (unsigned*)(img + IMG + 2 * 2 * 8 * 64 * 4);   // the next strip, broadcast
 
     // lane-derived values are re-derived from an opaque copy of threadIdx.x in every strip
     // iteration: hoisted out of the loop, their many per-lane addresses would stay live and spill
@@ -2209,10 +2221,18 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
         }
     };
 
-    // strips [s0, s1) of this workgroup: consecutive strips, so every workgroup gets a mix
-    // of full, edge and bottom-row strips
-    int sid = blockIdx.x * per;
-    const int s1 = min(sid + per, nstrip);
+    // Strips are dealt dynamically: workgroup b takes strips b and b + G (G = the grid,
+    // one workgroup per CU), then 2G + c for each c it draws from the counter `ctr`
+    // (zeroed by the launcher).  Workgroups start up to ~20 us apart and run at
+    // different speeds; a static deal of 8 strips each left ~11 % of the CUs idle and
+    // a ~20 us tail.  The draw for the strip after next is issued by lane 0 of wave 0
+    // right after a strip's first wait and counted as a vector-memory op; its answer is
+    // certain to have landed at the next strip's first wait (every DMA of that strip was
+    // issued after it), where it is broadcast through LDS.
+    const int G = (int)gridDim.x;
+    int sid = blockIdx.x;
+    int nsid = sid + G;                              // the strip after cur
+    unsigned drawn = 0u;                             // lane 0 of wave 0: the counter's last answer
     StripPos cur = pos_of(sid);
 #pragma unroll
     for (int j = 0; j < R; ++j) issue(cur, j, j, 0);
@@ -2233,7 +2253,7 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
     };
     const F8 id0 = ident(0), id1 = ident(1);
 
-    for (int it = 0; sid < s1; ++it, ++sid) {
+    for (int it = 0; sid < nstrip; ++it) {
         [[maybe_unused]] const int fa_sid = sid;
         FA_BSTAMP(0);
         tid = threadIdx.x;
@@ -2241,15 +2261,33 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
         lane = tid & 63; r = lane & 31; h = lane >> 5;
         g4 = lane >> 4; kh = g4 & 1; qq = (lane & 15) >> 2; pp = lane & 3;
         sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-        const bool has_next = sid + 1 < s1;
-        const StripPos nxt = has_next ? pos_of(sid + 1) : cur;
+        bool has_next = false;                       // set at the first wait (refills use it later)
+        StripPos nxt = cur;
         const int par = it & 1;
         auto slot_of = [&](int j) __attribute__((always_inline)) { return (gbase + j) & (R - 1); };
         // load j landed in every wave: its own DMA (counted wait), then the LDS barrier
         auto step_wait = [&](int j) __attribute__((always_inline)) {
             __builtin_amdgcn_sched_barrier(0);          // keep each step's work in its step (register pressure)
             wait_vm(vm_issued - mark_of(slot_of(j)));
+            if (j == 0 && it > 0 && wave == 0) {
+                asm volatile("" : "+v"(drawn));          // landed with this wait (see the deal above)
+                if (lane == 0) lds_w32u(nsid_lds, 2u * (unsigned)G + drawn);
+            }
             lds_barrier();
+            if (j == 0) {
+                if (it > 0) {
+                    nsid = (int)__builtin_bit_cast(unsigned, lds_b32(nsid_lds));
+                    lds_wait();
+                    asm volatile("" : "+v"(nsid));
+                    nsid = __builtin_amdgcn_readfirstlane(nsid);
+                }
+                has_next = nsid < nstrip;
+                nxt = has_next ? pos_of(nsid) : cur;
+                if (wave == 0) {                         // draw the strip after nsid
+                    if (lane == 0) drawn = atomic_add_ret(ctr, 1u);
+                    vm_issued += 1;
+                }
+            }
             FA_BSTAMP(1 + j);
         };
         // ring slot of load j is free: issue the load R later in the stream (this strip's, or the next's)
@@ -2495,6 +2533,8 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
                 }
         };
         // keys on lanes: oa[kb] = Σ A(f, queries) · xt[kb]
+        // this lane's two column masks (selects, not a lane-indexed array: that went to scratch)
+        const unsigned cmh0 = h ? cm[2] : cm[0], cmh1 = h ? cm[3] : cm[1];
         auto keys_out = [&](const u32x2 (&lo)[2][2], const u32x2 (&hi)[2][2], const F8 (&xt)[2][2][2], f32x16 (&oa)[2])
             __attribute__((always_inline)) {
 #pragma unroll
@@ -2505,8 +2545,7 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
             for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
                 for (int s_ = 0; s_ < 2; ++s_) {
-                    const u32x4 u = {lo[qb][s_][0] & cm[2 * h], lo[qb][s_][1] & cm[2 * h + 1], hi[qb][s_][0] & cm[2 * h],
-                                     hi[qb][s_][1] & cm[2 * h + 1]};
+                    const u32x4 u = {lo[qb][s_][0] & cmh0, lo[qb][s_][1] & cmh1, hi[qb][s_][0] & cmh0, hi[qb][s_][1] & cmh1};
                     const F8 af = __builtin_bit_cast(F8, u);
 #pragma unroll
                     for (int kb = 0; kb < 2; ++kb) oa[kb] = mfma32x32x16(af, xt[kb][qb][s_], oa[kb]);
@@ -2580,8 +2619,10 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
         }
         FA_BSTAMP(15);
         cur = nxt;
+        sid = nsid;
         gbase = (gbase + NA) & (R - 1);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last draw and stores retire before exit
 }
 
 // --------------------------------------------------------------------------
@@ -3341,16 +3382,25 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
     if (bwd_strip_ok(a)) {
         const int k0 = strip_first(a.g);
         const int64_t nsx = strip_count(a.g, k0), nstrip = nsx * a.g.O[1] * a.batch;
-        // persistent: one workgroup per CU, equal rounds of strips (no partial last round)
+        // persistent: one workgroup per CU, strips dealt by a counter in the workspace
         const int64_t cus = device_cus(s) > 0 ? device_cus(s) : 256;
-        const int64_t rounds = (nstrip + cus - 1) / cus, grid = (nstrip + rounds - 1) / rounds;
+        const int64_t grid = nstrip < cus ? nstrip : cus;
+        unsigned* const ctr = (unsigned*)a.workspace;
+        if (!ctr || a.workspace_bytes < 4) {
+            *why = "workspace missing (the strip backward keeps its strip counter there)";
+            return FA_ERR_WORKSPACE;
+        }
+        if ((e = hipMemsetAsync(ctr, 0, 4, s)) != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return FA_ERR_HIP;
+        }
         // strip ends on 16-B chunks: every strip boundary (k0 aligns them) and the covered right end
         const int64_t xend = a.g.O[0] * a.g.ws - a.g.pad;
         const bool aligned = ((k0 * a.g.ws - a.g.pad) % 8 + 8) % 8 == 0 && (xend >= a.g.S[0] || xend % 8 == 0);
 #define FA_BWD_STRIP2(DD, DVV, PA)                                                                              \
     hipLaunchKernelGGL((win_bwd_strip<T, DD, DVV, PA>), dim3((unsigned)grid), dim3(512), 0, s, (const T*)a.q,  \
                        (const T*)a.k, (const T*)a.v, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk, (T*)a.dv_, g, \
-                       (int)a.d, (int)a.dv, (int)nsx, k0, (int)nstrip, (int)rounds, a.scale, a.scale * kLog2e)
+                       (int)a.d, (int)a.dv, (int)nsx, k0, (int)nstrip, ctr, a.scale, a.scale * kLog2e)
 #define FA_BWD_STRIP(DD, DVV)                           \
     do {                                                \
         if (aligned) FA_BWD_STRIP2(DD, DVV, false);     \
