@@ -20,7 +20,10 @@
  * stream).  Calls are asynchronous on that stream, stateless, and safe from
  * concurrent host threads on distinct streams.  No call allocates device
  * memory, synchronises, or aborts: each returns FA_OK (0) or a nonzero
- * fa_status, with a thread-local message in fa_last_error().
+ * fa_status, with a thread-local message in fa_last_error().  A workspace
+ * belongs to one call at a time: calls that may run concurrently (distinct
+ * streams) need distinct workspaces (the backward kernels keep hand-off
+ * counters and strip counters in theirs).
  */
 #ifndef FA_HIP_H
 #define FA_HIP_H
