@@ -413,3 +413,36 @@ def test_windowed_backward_strip_full_size(fa):
             x = sl(a)
             err = np.abs(x - b_).max() / max(np.abs(b_).max(), 1e-2)
             assert np.all(np.isfinite(x)) and err <= 2e-2, f"image {b} {nm}: {err:.2e}"
+
+
+@pytest.mark.parametrize("B", [9, 40])
+def test_windowed_backward_strip_dynamic_deal_every_image(fa, B):
+    """The strip backward's dynamic deal (one workgroup per CU; strips b, b + G, then a
+    counter in the workspace) at strip counts that are not a multiple of the grid:
+    B = 9 (513 strips: 256 static first strips, 256 second, one drawn) and B = 40 (2280
+    strips: 1768 drawn, a ragged last round).  Every image of the default path's
+    gradients must match the one-window kernel (mode 3) within the 16-bit tolerance
+    (a strip the deal skipped would keep whatever the fresh output buffer held).  Run
+    twice: which workgroup draws which strip changes from run to run, the gradients
+    must not (bitwise)."""
+    W = H = 128
+    d = 64
+    g = torch.Generator(device="cuda").manual_seed(11 + B)
+    q, k, v, dy = (fa.jl_tensor(torch.randn((W, H, d, B), generator=g, device="cuda"), torch.bfloat16)
+                   for _ in range(4))
+    y, l, m = fa.windowed_fa(q, k, v, 7)
+    runs = [[t.clone() for t in fa.windowed_fa_backward(q, k, v, y, dy, l, m, 7)] for _ in range(2)]
+    torch.cuda.synchronize()
+    L = fa.lib()
+    old = L.fa_debug_set_win_composed(3)
+    try:
+        ref = fa.windowed_fa_backward(q, k, v, y, dy, l, m, 7)
+        torch.cuda.synchronize()
+    finally:
+        L.fa_debug_set_win_composed(old)
+    for a, a2, r, nm in zip(runs[0], runs[1], ref, ("dq", "dk", "dv")):
+        assert torch.equal(a, a2), f"{nm}: two runs of the dynamic deal differ"
+        x, xr = a.float(), r.float()
+        assert torch.isfinite(x).all(), f"{nm}: non-finite gradient (a strip not computed?)"
+        per_image = ((x - xr).abs().amax(dim=(0, 1, 2)) / xr.abs().amax(dim=(0, 1, 2)).clamp_min(1e-2))
+        assert float(per_image.max()) <= 2e-2, f"{nm}: worst image {int(per_image.argmax())} err {float(per_image.max()):.2e}"
