@@ -1470,7 +1470,10 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
             }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's V DMA (and the l, m stores)
+    // this wave's V DMA (and the l, m stores).  The builtin, not asm: hipcc then knows no
+    // LDS-DMA is pending, and adds no vmcnt(0) of its own before the epilogue's LDS
+    // accesses (which made chunk 1's image reads wait for chunk 0's y stores).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     lds_barrier();                                       // every wave's V landed
     FA_STAMP(3);
 
