@@ -300,7 +300,13 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
     t_f = e_f / steps_fwd
     _, e_b = time_region(lambda: fa.dense_fa_backward(Q, K, V, O, dO, l, m), steps_bwd, 1, dist)
     t_b = e_b / steps_bwd
-    hs = fa.backward_handoff_status(Q.device)
+    hs = fa.backward_handoff_status(Q.device)   # the last timed call
+    # each call's pre-pass rewrites the status word, so the earlier timed calls are
+    # re-checked one by one in an untimed pass: any timeout marks the block tainted
+    hs_calls = []
+    for _ in range(steps_bwd):
+        fa.dense_fa_backward(Q, K, V, O, dO, l, m)
+        hs_calls.append(fa.backward_handoff_status(Q.device))
     res = {
         "workload": "configs[3]: dense_fa bf16 forward + backward, (B,H,N,d)=(4,16,8192,128)",
         "fwd_tflops": f / t_f / 1e12, "bwd_tflops": 2.5 * f / t_b / 1e12,
@@ -314,6 +320,8 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
         "roofline_fwd_bwd": _mfma_roofline(3.5 * f, t_f + t_b, "forward + backward calls"),
         "bwd_handoff": {-1: "two-pass plan (no hand-off)", 0: "single pass, hand-off completed",
                         1: "single pass, hand-off TIMED OUT: dQ recomputed by the guarded pass"}.get(hs, hs),
+        "bwd_handoff_recheck": hs_calls,
+        "bwd_fallback_tainted": any(x == 1 for x in hs_calls + [hs]),
     }
     del Q, K, V, dO, O, l, m
     torch.cuda.empty_cache()

@@ -103,10 +103,11 @@ int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
 // benchmarking: 0 = auto (per head-dim class), 4..7 = {waves, query blocks per
 // wave} = {4,1}, {8,1}, {4,2}, {8,2} on 32x32x16 MFMA; 8, 9 = 8 waves x
 // {64, 32} query rows on 16x16x32 MFMA; 16 = 8 waves x 32 rows at 4 waves per SIMD;
-// 20 = the default geometries with per-element Q gathers and O stores.
+// 20 = the default geometries with per-element Q gathers and O stores; 30 = the
+// one-wave-per-SIMD persistent kernel (fa_fwd_p4.hip) where its shape rules allow.
 int fa_debug_set_fwd_variant(int v) {
     const int old = fa::g_fwd_variant;
-    if (v == 0 || (v >= 4 && v <= 9) || v == 16 || v == 20) fa::g_fwd_variant = v;
+    if (v == 0 || (v >= 4 && v <= 9) || v == 16 || v == 20 || v == 30) fa::g_fwd_variant = v;
     return old;
 }
 

@@ -1181,16 +1181,22 @@ static SplitPlan split_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
 // --------------------------------------------------------------------------
 // launcher
 // --------------------------------------------------------------------------
+bool launch_dense_fwd_p4(const FwdParams& p, int Dc, int DVc, int dtype, hipStream_t s, hipError_t* err);
+
 template <class T, int D>
 static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
+    if (p.fast && g_fwd_variant == 30) {   // one wave per SIMD, persistent (fa_fwd_p4.hip)
+        hipError_t e = hipSuccess;
+        if (launch_dense_fwd_p4(p, D, DVc, std::is_same<T, bf16>::value ? FA_DTYPE_BF16 : FA_DTYPE_F16, s, &e)) return e;
+    }
     if (p.fast) {
         // geometry per head-dim class (measured on MI355X):
         // <= 64: 8 waves x 2 query blocks (512 rows / workgroup); 128: 8 waves x 1.
         int v = g_fwd_variant;
         // default geometries stage Q / O through LDS when the shape allows (variant 20:
         // the same geometries with per-element Q gathers / O stores, for A/B)
-        const bool wide = p.wide && (v == 0 || v == 5 || v == 7);
-        if (v == 0 || v == 20) v = (D <= 64 && DVc <= 64) ? 7 : 5;
+        const bool wide = p.wide && (v == 0 || v == 5 || v == 7 || v == 30);
+        if (v == 0 || v == 20 || v == 30) v = (D <= 64 && DVc <= 64) ? 7 : 5;
         const int nw = (v == 4 || v == 6) ? 4 : 8;
         // query rows per workgroup (split kernels: 512 for w8q2 / t16q4, 256 for w8b64 / t16q2)
         const int rows = v == 8 ? 512 : v == 9 ? 256 : v == 16 ? 256 : 32 * nw * (v >= 6 ? 2 : 1);

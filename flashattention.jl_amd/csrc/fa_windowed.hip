@@ -3388,8 +3388,11 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
         // persistent: one workgroup per CU, strips dealt by a counter in the workspace
         const int64_t cus = device_cus(s) > 0 ? device_cus(s) : 256;
         const int64_t grid = nstrip < cus ? nstrip : cus;
-        unsigned* const ctr = (unsigned*)a.workspace;
-        if (!ctr || a.workspace_bytes < 4) {
+        // the counter is an atomic word: round its address up to 256 B as the dense
+        // backward does (the header allows any workspace alignment; windowed_workspace
+        // reserves the 256-B slack)
+        unsigned* const ctr = (unsigned*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
+        if (!a.workspace || a.workspace_bytes < (size_t)((char*)ctr - (char*)a.workspace) + 4) {
             *why = "workspace missing (the strip backward keeps its strip counter there)";
             return FA_ERR_WORKSPACE;
         }

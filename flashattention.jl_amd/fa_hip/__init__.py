@@ -381,7 +381,7 @@ def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
     dV = jl_empty((Nk, dv, B), Q.dtype, Q.device)
     L = lib()
     nws = L.fa_dense_bwd_workspace(code, N, Nk, d, dv, B)
-    ws = _workspace(Q.device, nws)
+    ws = _workspace(Q.device, nws, entry="dense_fa_backward")
     _check(L.fa_dense_bwd(code, _ptr(Q), _ptr(K), _ptr(V), _ptr(O), _ptr(dO), _ptr(l), _ptr(m),
                           _ptr(dQ), _ptr(dK), _ptr(dV), N, Nk, d, dv, B, float(scale),
                           _ptr(ws), int(nws), _stream(Q)))
@@ -394,12 +394,15 @@ def backward_handoff_status(device=None) -> int:
     scratch buffer).  Synchronises that stream.  -1: the two-pass form ran (no
     hand-off); 0: single pass, every dQ hand-off completed; 1: a hand-off timed out
     and dQ was recomputed by the guarded pass (same values within rounding, other
-    bits, up to ~20 ms slower).  Raises FlashAttentionError when another entry point
-    has used the scratch buffer since."""
+    bits, up to ~20 ms slower).  Raises FlashAttentionError when no dense_fa_backward
+    has run on this stream, or when another entry point has taken the scratch buffer
+    since (the module records the last entry point per (device, stream))."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     stream = torch.cuda.current_stream(device)
-    buf = _WS.get((device.type, device.index, stream.cuda_stream))
-    _require(buf is not None, "no backward has run on this stream")
+    key = (device.type, device.index, stream.cuda_stream)
+    buf = _WS.get(key)
+    _require(buf is not None and _WS_LAST.get(key) == "dense_fa_backward",
+             "the last call that used this stream's scratch buffer was not dense_fa_backward")
     st = ctypes.c_int(-2)
     _check(lib().fa_dense_bwd_handoff_status(_ptr(buf), buf.numel(), ctypes.c_void_p(stream.cuda_stream),
                                              ctypes.byref(st)))
@@ -417,9 +420,10 @@ def window_geometry(spatial: Sequence[int], ws: int, stride: int, pad: int):
 
 
 _WS = {}
+_WS_LAST = {}   # (device, stream) -> name of the entry point that last took the scratch buffer
 
 
-def _workspace(device, nbytes: int) -> torch.Tensor:
+def _workspace(device, nbytes: int, entry: str = "other") -> torch.Tensor:
     """Scratch buffer for the C ABI's workspace arguments, one per (device,
     stream), grown on demand.
 
@@ -432,6 +436,7 @@ def _workspace(device, nbytes: int) -> torch.Tensor:
     one stream run in order, so reusing it across calls is safe."""
     stream = torch.cuda.current_stream(device)
     key = (device.type, device.index, stream.cuda_stream)
+    _WS_LAST[key] = entry
     buf = _WS.get(key)
     if buf is None or buf.numel() < max(int(nbytes), 1):
         with torch.cuda.stream(stream):

@@ -23,7 +23,10 @@
  * fa_status, with a thread-local message in fa_last_error().  A workspace
  * belongs to one call at a time: calls that may run concurrently (distinct
  * streams) need distinct workspaces (the backward kernels keep hand-off
- * counters and strip counters in theirs).
+ * counters and strip counters in theirs).  A workspace may start at any
+ * address: the *_workspace() sizes include 256 bytes of slack, and every entry
+ * point rounds the addresses of its counters and staging buffers up to 256 B
+ * inside it.
  */
 #ifndef FA_HIP_H
 #define FA_HIP_H

@@ -14,6 +14,8 @@ import sys
 import time
 
 import numpy as np
+import pytest
+import torch
 import torch.multiprocessing as mp
 
 import bench
@@ -98,6 +100,11 @@ def _bench_env(**extra):
     return env
 
 
+# the CPU step hook (FA_BENCH_CPU_STEP) is refused where a GPU is visible
+_cpu_only = pytest.mark.skipif(torch.cuda.is_available(), reason="CPU step hook: refused on a GPU box")
+
+
+@_cpu_only
 def test_bench_gpus_2_literal_command_spawns_two_ranks():
     """The driver's literal form `python bench.py --gpus 2` (no torch.distributed.run
     around it) starts two ranks itself; with the CPU step hook (rank r sleeps
@@ -124,6 +131,7 @@ def test_bench_gpus_2_literal_command_spawns_two_ranks():
     assert abs(out["value"] - 2 * flops_rank * 4 / (out["ms_per_step"] * 4 / 1e3) / 1e12) < 1e-6 * out["value"]
 
 
+@_cpu_only
 def test_bench_refuses_gpus_world_mismatch():
     """Under torch.distributed.run, --gpus must equal WORLD_SIZE (exit 2), and
     --gpus < 1 is refused, before anything is measured."""
