@@ -33,13 +33,17 @@
 // Taken for the LDS-staged fast shapes (bf16/f16, Nk % 8 == 0, N % 8 == 0, 16-B
 // aligned tensors), d = dv = 64 or 128, at least one block per CU and enough key
 // tiles per block for the Q prefetch (launch_dense_fwd_p4).
+#include <type_traits>
+
 #include "fa_common.h"
 #include "fa_internal.h"
 #include "fa_fwd_params.h"
 #include "../../include/fa_hip.h"
 
+// Diagnostic hooks (tools/exp/p4_lab.hip; empty in the product build):
+// FA_P4_STAMP(point, tile) records s_memtime at a phase boundary.
 #ifndef FA_P4_STAMP
-#define FA_P4_STAMP(k)
+#define FA_P4_STAMP(pt, j)
 #endif
 
 namespace fa {
@@ -112,6 +116,16 @@ struct P4 {
     static_assert(LDSB <= 163840, "LDS budget");
 };
 
+// Compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1 (every index
+// is a constant, whatever the body's size; #pragma unroll may stop short of a full
+// unroll of a big body and leave register arrays dynamically indexed, i.e. in scratch).
+template <class F, int... I>
+__device__ __forceinline__ void p4_static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void p4_static_for(F&& f) { p4_static_for_impl(f, std::make_integer_sequence<int, N>{}); }
+
 // Q image position of logical byte `lb` (= 2 x token) of feature row f (the qo_at of
 // dense_fwd_tiled at 256 rows): 32-B blocks XOR (f & 3) | (bit 2 of f) << 2.
 __device__ __forceinline__ int p4_qpos(int f, int lb) {
@@ -119,55 +133,65 @@ __device__ __forceinline__ int p4_qpos(int f, int lb) {
     return f * (kP4Rows * 2) + (((lb >> 5) ^ X) << 5) + (lb & 31);
 }
 
-// Register fences: an empty volatile asm that "redefines" a value pins the work that
-// produces it before that point and the work that consumes it after (volatile asm
-// keeps its order against the MFMA and DMA asm).  Fencing a private value costs
-// nothing; work whose inputs are shared (the scores) is pinned through a scalar
-// operand fenced at its slot (an s_mov, no vector issue).
-__device__ __forceinline__ void p4_pin(float& x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ float p4_pin_s(float x) { asm volatile("" : "+s"(x)); return x; }
-template <class V> __device__ __forceinline__ void p4_pin_vec(V& x) { asm volatile("" : "+v"(x)); }
+// The softmax and row-max VALU work is written as inline asm, one short statement per
+// step: volatile asm keeps program order against the MFMA asm, so each step stays in
+// the MFMA slot it is written in (compiler-generated arithmetic floats across
+// sched_barrier, and pinning it with register fences costs s_nop / s_mov per fence).
+// Hazards inside the hot loop are the kernel's: an exponential's consumer is never the
+// next instruction (part1 of chunk c follows part0 of chunk c+1), and the scores an
+// asm MFMA writes are read a phase later.
+template <class T> struct P4Cvt;
+template <> struct P4Cvt<bf16> { static constexpr const char* op = "v_cvt_pk_bf16_f32"; };
+template <> struct P4Cvt<f16> { static constexpr const char* op = "v_cvt_pk_f16_f32"; };
+
+__device__ __forceinline__ void p4_exp2x2(float& e0, float& e1, float s0, float s1, float c, float nmc) {
+    float t0, t1;
+    asm volatile("v_fma_f32 %2, %4, %6, %7\n\tv_fma_f32 %3, %5, %6, %7\n\tv_exp_f32 %0, %2\n\tv_exp_f32 %1, %3"
+                 : "=&v"(e0), "=&v"(e1), "=&v"(t0), "=&v"(t1)
+                 : "v"(s0), "v"(s1), "s"(c), "v"(nmc));
+}
+template <class T>
+__device__ __forceinline__ unsigned p4_pack(float e0, float e1) {
+    unsigned r;
+    if constexpr (std::is_same<T, bf16>::value) asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(e0), "v"(e1));
+    else asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(e0), "v"(e1));
+    return r;
+}
+__device__ __forceinline__ void p4_add2(float& a0, float& a1, float e0, float e1) {
+    asm volatile("v_add_f32 %0, %0, %2\n\tv_add_f32 %1, %1, %3" : "+v"(a0), "+v"(a1) : "v"(e0), "v"(e1));
+}
+__device__ __forceinline__ float p4_max3(float a, float b, float c) {
+    float r;
+    asm volatile("v_maximum3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // The softmax of one query block's 64 scores per lane pair (32 per lane), cut into
 // 16 chunks of two scores, each in two parts: part 0 = two FMAs (c·s − c·m) and two
-// exponentials, part 1 = the two sum adds and the bf16/f16 pack.
+// exponentials, part 1 = the two sum adds and the bf16/f16 pack into P (dword view).
 template <class T>
 struct SoftmaxQB {
-    typedef typename Frag8<T>::type F8;
-    float mc, c;
+    float nmc, c;    // −c·m_used, c
     float e[2][2];   // exponentials of chunk c in e[c & 1]
     float ps[4];
     __device__ __forceinline__ void part0(const f32x16 (&S)[2], int ch) {
         const int kb = ch >> 3, x = 2 * (ch & 7);
-        float* ee = e[ch & 1];
-        const float cs = p4_pin_s(c);   // c is uniform (SGPR); the running max is per lane
-        ee[0] = exp2_fast(fmaf(S[kb][x], cs, -mc));
-        ee[1] = exp2_fast(fmaf(S[kb][x + 1], cs, -mc));
-        p4_pin(ee[0]);
-        p4_pin(ee[1]);
+        p4_exp2x2(e[ch & 1][0], e[ch & 1][1], S[kb][x], S[kb][x + 1], c, nmc);
     }
-    __device__ __forceinline__ void part1(F8 (&P)[2][2], int ch) {
+    __device__ __forceinline__ void part1(u32x4 (&P)[2][2], int ch) {
         const int kb = ch >> 3, x = 2 * (ch & 7);
-        float* ee = e[ch & 1];
-        p4_pin(ee[0]);
-        p4_pin(ee[1]);
+        const float e0 = e[ch & 1][0], e1 = e[ch & 1][1];
         if (ch < 2) {   // the first four exponentials seed the partial sums
-            ps[x & 3] = ee[0];
-            ps[(x + 1) & 3] = ee[1];
+            ps[x & 3] = e0;
+            ps[(x + 1) & 3] = e1;
         } else {
-            ps[x & 3] += ee[0];
-            ps[(x + 1) & 3] += ee[1];
+            p4_add2(ps[x & 3], ps[(x + 1) & 3], e0, e1);
         }
-        p4_pin(ps[x & 3]);
-        p4_pin(ps[(x + 1) & 3]);
-        P[kb][x >> 3][x & 7] = (T)ee[0];
-        P[kb][x >> 3][(x & 7) + 1] = (T)ee[1];
-        if ((x & 7) == 6) p4_pin_vec(P[kb][x >> 3]);
+        P[kb][x >> 3][(x & 7) >> 1] = p4_pack<T>(e0, e1);
     }
     // part k of 32 in issue order: part0 of chunk 0, then (part0 of chunk c+1, part1
-    // of chunk c) pairs, then part1 of chunk 15 — an exponential's consumer never
-    // follows it directly (the trans-use wait state)
-    __device__ __forceinline__ void part(const f32x16 (&S)[2], F8 (&P)[2][2], int k) {
+    // of chunk c) pairs, then part1 of chunk 15
+    __device__ __forceinline__ void part(const f32x16 (&S)[2], u32x4 (&P)[2][2], int k) {
         if (k == 0) part0(S, 0);
         else if (k == 31) part1(P, 15);
         else if (k & 1) part0(S, (k + 1) >> 1);
@@ -176,28 +200,18 @@ struct SoftmaxQB {
     __device__ __forceinline__ float sum() const { return (ps[0] + ps[1]) + (ps[2] + ps[3]); }
 };
 
-// Lane maximum of one query block's 32 scores in 18 steps: four v_maximum3 chains
-// seeded with two scores each (steps 0-3), twelve chain steps of two scores, then
-// the combine (steps 16, 17 leave the result in mt).
+// Lane maximum of one query block's 32 scores in 16 v_maximum3 steps: four chains
+// seeded with three scores each (steps 0-3), ten chain steps of two scores, then the
+// combine (steps 14, 15 leave the result in mt).
 struct MaxQB {
     float a[4], t, mt;
-    static constexpr int NOPS = 18;
+    static constexpr int NOPS = 16;
     __device__ __forceinline__ void op(const f32x16 (&S)[2], int m) {
         auto v = [&](int k) { return S[k >> 4][k & 15]; };
-        if (m < 4) {
-            a[m] = vmax3(v(2 * m), v(2 * m + 1), p4_pin_s(kNegInf));
-            p4_pin(a[m]);
-        } else if (m < 16) {
-            const int k = 8 + 2 * (m - 4), cc = m & 3;
-            p4_pin(a[cc]);
-            a[cc] = vmax3(a[cc], v(k), v(k + 1));
-            p4_pin(a[cc]);
-        } else if (m == 16) {
-            t = vmax3(a[0], a[1], a[2]);
-            p4_pin(t);
-        } else {
-            mt = vmax(t, a[3]);
-        }
+        if (m < 4) a[m] = p4_max3(v(3 * m), v(3 * m + 1), v(3 * m + 2));
+        else if (m < 14) { const int k = 12 + 2 * (m - 4), cc = m & 3; a[cc] = p4_max3(a[cc], v(k), v(k + 1)); }
+        else if (m == 14) t = p4_max3(a[0], a[1], a[2]);
+        else mt = p4_max3(t, a[3], a[3]);
     }
 };
 
@@ -268,180 +282,195 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
     const uint32_t kbytes = (uint32_t)(ldk * d * (int)sizeof(T)), vbytes = (uint32_t)(ldk * dv * (int)sizeof(T));
     const uint32_t qbytes = (uint32_t)(N * d * (int)sizeof(T));
     // a slab's K / V base; blocks past the end get a zero-length descriptor (reads → 0)
-    auto kbase_of = [&](int id) { return (const T*)p.K + (int64_t)(id < nblk ? id / nqb : 0) * ldk * d; };
-    auto vbase_of = [&](int id) { return (const T*)p.V + (int64_t)(id < nblk ? id / nqb : 0) * ldk * dv; };
+    auto kbase_of = [&](int id) __attribute__((always_inline)) { return (const T*)p.K + (int64_t)(id < nblk ? id / nqb : 0) * ldk * d; };
+    auto vbase_of = [&](int id) __attribute__((always_inline)) { return (const T*)p.V + (int64_t)(id < nblk ? id / nqb : 0) * ldk * dv; };
     // K tile `j` of the slab behind `ds` into K slot `slot`
-    auto dma_k1 = [&](const u32x4& ds, int slot, int j, int it) {
+    auto dma_k1 = [&](const u32x4& ds, int slot, int j, int it) __attribute__((always_inline)) {
         p4_dma(ds, lds0 + C::KOFF + slot * C::KSLOT + (it * 4 + wave) * 1024, kgo[it], j * 128);
     };
-    auto dma_v1 = [&](const u32x4& ds, int slot, int j, int it) {
+    auto dma_v1 = [&](const u32x4& ds, int slot, int j, int it) __attribute__((always_inline)) {
         p4_dma(ds, lds0 + C::VOFF + slot * C::VSLOT + (it * 4 + wave) * 1024, vgo[it], j * 128);
     };
     // piece `it` of the Q image of the block whose Q slab is `ds` and query block qb;
     // `dst` = the piece's place in the image (or a scratch place: see phase B)
-    auto dma_q1 = [&](const u32x4& ds, int qb, int it, uint32_t dst) {
+    auto dma_q1 = [&](const u32x4& ds, int qb, int it, uint32_t dst) __attribute__((always_inline)) {
         p4_dma(ds, dst, qgo, it * 16 * N + qb * (kP4Rows * 2));
     };
-    auto qdst = [&](int it) { return lds0 + C::QOFF + (uint32_t)(it * 4 + wave) * 1024u; };
+    auto qdst = [&](int it) __attribute__((always_inline)) { return lds0 + C::QOFF + (uint32_t)(it * 4 + wave) * 1024u; };
 
     F8 qf[2][C::NKS];
     f32x16 oacc[2][C::NCB];
+    f32x16 S[2][2];        // [query block][key block]: one score tile per query block
+    u32x4 P[2][2][2];      // [query block][key block][k-step], packed P (dword view of the bf16x8 operand)
     float m_used[2], m_true[2], l_run[2];
-    f32x16 sA[2][2], sB[2][2];
-    F8 pA0[2][2], pB0[2][2], p1[2][2];
 
-    // ---- phase A: S = K(slot)·Qᵀ, each MFMA followed by valu(slot index) ----
-    auto phaseA = [&](f32x16 (&S)[2][2], const char* kslot, auto&& valu) {
-        F8 kf[3];
-        // the lane offsets re-enter here (opaque), so the per-read addresses are one
-        // base + immediate each instead of ~70 loop-invariant VGPRs the compiler would
-        // hoist out of the tile loop (and spill)
+    // ---- one phase: the MFMAs of query block u — Sᵀ_u = K·Qᵀ_u (QK) then Oᵀ_u += Vᵀ·Pᵀ_u
+    // (PV) — with valu(slot) after each MFMA and mid() before MFMA slot NPRE.  The LDS
+    // operands stream two fragments ahead; sched_barrier(0) fences every slot.
+    auto phase = [&](auto QKt, auto PVt, auto NPREt, int u, const char* kslot, const char* vslot, auto&& valu,
+                     auto&& mid) __attribute__((always_inline)) {
+        constexpr bool QK = decltype(QKt)::value, PV = decltype(PVt)::value;
+        constexpr int NPRE = decltype(NPREt)::value;
+        constexpr int NKQ = QK ? C::NKQ : 0;
+        constexpr int NM = NKQ + (PV ? C::NVQ : 0);
+        // the lane offsets re-enter here (opaque), so each read is one base + immediate
+        // instead of ~70 loop-invariant address VGPRs the compiler would hoist and spill
         int ko[2] = {koff[0], koff[1]};
-        asm volatile("" : "+v"(ko[0]), "+v"(ko[1]));
-        auto rd = [&](int i) {
-            const int kb = i / C::NKS, s = i % C::NKS;
-            const char* a = kslot + ko[kb] + 16 * s * 128;
-            const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
-            const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
-            kf[i % 3] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        };
-        rd(0);
-        rd(1);
-        p4_fence();
-#pragma unroll
-        for (int i = 0; i < C::NKQ; ++i) {
-            const int kb = i / C::NKS, s = i % C::NKS;
-            if (i + 2 < C::NKQ) rd(i + 2);
-            p4_mfma_s(S[0][kb], kf[i % 3], qf[0][s], s == 0);
-            valu(2 * i);
-            p4_mfma_s(S[1][kb], kf[i % 3], qf[1][s], s == 0);
-            valu(2 * i + 1);
-            p4_fence();
-        }
-    };
-    // ---- phase B: Oᵀ += Vᵀ(slot)·Pᵀ, each MFMA followed by valu(slot index) ----
-    auto phaseB = [&](const char* vslot, const F8 (&P0)[2][2], const F8 (&P1)[2][2], auto&& valu) {
-        F8 vf[3];
         int vo[2][2] = {{voff[0][0], voff[0][1]}, {voff[1][0], voff[1][1]}};
-        asm volatile("" : "+v"(vo[0][0]), "+v"(vo[0][1]), "+v"(vo[1][0]), "+v"(vo[1][1]));
-        auto rd = [&](int i) {
-            const int cb = i >> 2, kb = (i >> 1) & 1, s = i & 1;
-            vf[i % 3] = *(const F8*)(vslot + cb * 32 * 128 + vo[kb][s]);
+        asm volatile("" : "+v"(ko[0]), "+v"(ko[1]), "+v"(vo[0][0]), "+v"(vo[0][1]), "+v"(vo[1][0]), "+v"(vo[1][1]));
+        F8 fr[3];
+        auto rd = [&](int i) __attribute__((always_inline)) {
+            if (i < NKQ) {
+                const int kb = i / C::NKS, s = i % C::NKS;
+                const char* a = kslot + ko[kb] + 16 * s * 128;
+                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+                const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
+                fr[i % 3] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            } else {
+                const int j = i - NKQ, cb = j >> 2, kb = (j >> 1) & 1, s = j & 1;
+                fr[i % 3] = *(const F8*)(vslot + cb * 32 * 128 + vo[kb][s]);
+            }
         };
         rd(0);
-        rd(1);
+        if (NM > 1) rd(1);
         p4_fence();
-#pragma unroll
-        for (int i = 0; i < C::NVQ; ++i) {
-            const int cb = i >> 2, kb = (i >> 1) & 1, s = i & 1;
-            if (i + 2 < C::NVQ) rd(i + 2);
-            oacc[0][cb] = mfma32x32x16(vf[i % 3], P0[kb][s], oacc[0][cb]);
-            valu(2 * i);
-            oacc[1][cb] = mfma32x32x16(vf[i % 3], P1[kb][s], oacc[1][cb]);
-            valu(2 * i + 1);
+        p4_static_for<NM>([&](auto It) __attribute__((always_inline)) {
+            constexpr int i = decltype(It)::value;
+            if constexpr (i == NPRE) {
+                mid();
+                p4_fence();
+            }
+            if constexpr (i + 2 < NM) rd(i + 2);
+            if constexpr (i < NKQ) {
+                constexpr int kb = i / C::NKS, s = i % C::NKS;
+                p4_mfma_s(S[u][kb], fr[i % 3], qf[u][s], s == 0);
+            } else {
+                constexpr int j = i - NKQ, cb = j >> 2, kb = (j >> 1) & 1, s = j & 1;
+                oacc[u][cb] = mfma32x32x16(fr[i % 3], __builtin_bit_cast(F8, P[u][kb][s]), oacc[u][cb]);
+            }
+            valu(i);
             p4_fence();
+        });
+        if constexpr (NPRE >= NM) mid();
+    };
+    auto none = [](int) __attribute__((always_inline)) {};
+    auto nomid = []() __attribute__((always_inline)) {};
+
+    // the lazy-rescale decision for query block v after its tile max: the running max
+    // used for the exponentials is raised only when some lane's tile max exceeds it by
+    // more than the threshold (a wave-uniform branch); O_v's last MFMAs ran in the
+    // previous phase, l_v and O_v are scaled together.  m_used starts at −inf, so the
+    // first tile always takes the branch (scaling O = 0, l = 0 by 0).
+    auto decide = [&](int v, float mt) __attribute__((always_inline)) {
+        m_true[v] = vmax(m_true[v], mt);
+        if (__builtin_amdgcn_ballot_w64(mt > m_used[v] + thr_raw) != 0) {
+            const float mn = fmaxf(m_used[v], swap_halves_max(mt));
+            const float al = exp2_fast((m_used[v] - mn) * c);
+            l_run[v] *= al;
+#pragma unroll
+            for (int cb = 0; cb < C::NCB; ++cb)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) oacc[v][cb][x] *= al;
+            m_used[v] = mn;
         }
     };
-    auto no_valu = [](int) {};
 
-    auto softmax_p = [&](const f32x16 (&S)[2], float mused, F8 (&P)[2][2]) -> float {
-        SoftmaxQB<T> sm;
-        sm.c = c;
-        sm.mc = mused * c;
+    // The VALU side of a phase for query block v: its tile max in the first NPRE MFMA
+    // slots, the decision, then its softmax (P_v, l_v) over the remaining slots.
+    // NM = MFMA slots of the phase.
+    auto softmax_side = [&](auto NMt, auto NPREt, int v, MaxQB& mx, SoftmaxQB<T>& sm) __attribute__((always_inline)) {
+        constexpr int NM = decltype(NMt)::value, NPRE = decltype(NPREt)::value;
+        return [&, v](int i) __attribute__((always_inline)) {
+            if (i < NPRE) {
 #pragma unroll
-        for (int ch = 0; ch < 16; ++ch) {
-            sm.part0(S, ch);
-            sm.part1(P, ch);
-        }
-        return sm.sum();
+                for (int m = MaxQB::NOPS * i / NPRE; m < MaxQB::NOPS * (i + 1) / NPRE; ++m) mx.op(S[v], m);
+            } else {
+                const int k = i - NPRE;
+#pragma unroll
+                for (int part = 32 * k / (NM - NPRE); part < 32 * (k + 1) / (NM - NPRE); ++part) sm.part(S[v], P[v], part);
+            }
+        };
     };
 
     // per-block DMA context: this block's and the next block's slabs
+    int p4_blk = 0;   // block counter of this workgroup (read by the diagnostic stamps only)
+    (void)p4_blk;
     const T *kp0 = nullptr, *kp1 = nullptr, *vp0 = nullptr, *vp1 = nullptr, *qpn = nullptr;
     uint32_t kn1 = 0, vn1 = 0, qnn = 0;   // the next block's descriptor lengths (0: none)
     int qbn = 0;
 
-    // One pipelined tile j (K slot of tile j+1 = ksl1, of tile j = ksl0; V slot vsl):
-    // Sc = S(j) with query block 0 already in Pc0; leaves Sn = S(j+1) and Pn0.
-    auto step = [&](int j, int ksl0, int ksl1, int vsl, f32x16 (&Sc)[2][2], f32x16 (&Sn)[2][2], F8 (&Pc0)[2][2],
-                    F8 (&Pn0)[2][2]) {
-        // ---- phase A(j): Sn = K(j+1)·Qᵀ ∥ softmax of Sc, query block 1 ----
-        {
+    typedef std::integral_constant<bool, true> Yes;
+    typedef std::integral_constant<bool, false> No;
+    constexpr int NMF = C::NKQ + C::NVQ;              // MFMA slots of a full phase
+    constexpr int NPRE = NMF >= 32 ? 6 : 4;           // slots carrying the max chains
+    typedef std::integral_constant<int, NMF> NMt;
+    typedef std::integral_constant<int, NPRE> NPt;
+    typedef std::integral_constant<int, C::NVQ> NMvt;  // PV-only phase (last tile)
+    typedef std::integral_constant<int, (C::NVQ >= 16 ? 4 : 2)> NPvt;
+
+    // One tile t (block tile j): X = query block 0's MFMAs ∥ block 1's softmax of tile
+    // j; Y = block 1's MFMAs ∥ block 0's softmax of tile j+1.  DMA: the next V tile and
+    // the next block's Q piece in X, the K tile three ahead in Y; then the wait for
+    // everything but that K tile, and the tile's barrier.
+    auto tile = [&](auto LASTt, int j, int ks1, int ks0, int vs0) __attribute__((always_inline)) {
+        constexpr bool LAST = decltype(LASTt)::value;
+        const char* kslot = kring + ks1 * C::KSLOT;   // K(j+1)
+        const char* vslot = vring + vs0 * C::VSLOT;   // V(j)
+        // DMA targets: V(j+1) → the other V slot, K(j+3) → the slot of K(j)
+        const int jv = j + 1, jk = j + 3;
+        const bool vn = jv >= NT, kn = jk >= NT;
+        const u32x4 vds = p4_desc(vn ? vp1 : vp0, vn ? vn1 : vbytes), kds = p4_desc(kn ? kp1 : kp0, kn ? kn1 : kbytes);
+        const int jv2 = vn ? jv - NT : jv, jk2 = kn ? jk - NT : jk;
+        FA_P4_STAMP(2, j);
+        {   // ---- X: block 0 MFMAs ∥ block 1 softmax (tile j) ----
+            MaxQB mx;
             SoftmaxQB<T> sm;
             sm.c = c;
-            sm.mc = m_used[1] * c;
-            phaseA(Sn, kring + ksl1 * C::KSLOT, [&](int slot) {
-                constexpr int NS = 2 * C::NKQ;   // MFMA slots: softmax parts [32 slot / NS, 32 (slot + 1) / NS)
-#pragma unroll
-                for (int part = 32 * slot / NS; part < 32 * (slot + 1) / NS; ++part) sm.part(Sc[1], p1, part);
-            });
+            auto side = softmax_side(std::conditional_t<LAST, NMvt, NMt>{}, std::conditional_t<LAST, NPvt, NPt>{}, 1, mx, sm);
+            auto valu = [&](int i) __attribute__((always_inline)) {
+                side(i);
+                // V(j+1) pieces and the Q piece early in the phase
+                constexpr int NMx = LAST ? C::NVQ : NMF;
+                constexpr int NPx = LAST ? (C::NVQ >= 16 ? 4 : 2) : NPRE;
+                if (i >= NPx && i < NPx + C::VP) dma_v1(vds, vs0 ^ 1, jv2, i - NPx);
+                if (i == NPx + C::VP) {
+                    const bool qv = j < C::QP;
+                    dma_q1(p4_desc(qpn, qv ? qnn : 0u), qbn, qv ? j : 0, qv ? qdst(j) : lds0 + C::OOFF + (uint32_t)wave * C::OST);
+                }
+                (void)NMx;
+            };
+            auto mid = [&]() __attribute__((always_inline)) {
+                decide(1, mx.mt);
+                sm.nmc = -m_used[1] * c;
+            };
+            phase(std::integral_constant<bool, !LAST>{}, Yes{}, std::conditional_t<LAST, NPvt, NPt>{}, 0, kslot, vslot, valu, mid);
             l_run[1] += sm.sum();
         }
-        p4_wait_all_barrier();
-        // ---- phase B(j): O += V(j)·P(j) ∥ max of Sn, speculative softmax of Sn block 0, DMA ----
-        MaxQB mx0, mx1;
-        SoftmaxQB<T> sm;
-        sm.c = c;
-        sm.mc = m_used[0] * c;
-        // DMA of this phase: K(j+3) → slot ksl0, V(j+1) → the other V slot, Q piece j
-        const int jk = j + 3, jv = j + 1;
-        const bool kn = jk >= NT, vn = jv >= NT;
-        const u32x4 kds = p4_desc(kn ? kp1 : kp0, kn ? kn1 : kbytes), vds = p4_desc(vn ? vp1 : vp0, vn ? vn1 : vbytes);
-        const int jk2 = kn ? jk - NT : jk, jv2 = vn ? jv - NT : jv;
-        phaseB(vring + vsl * C::VSLOT, Pc0, p1, [&](int slot) {
-            constexpr int NS = 2 * C::NVQ;   // MFMA slots; softmax parts and max steps spread evenly
-            constexpr int NM = 2 * MaxQB::NOPS;
-#pragma unroll
-            for (int m = NM * slot / NS; m < NM * (slot + 1) / NS; ++m) {
-                if (m < MaxQB::NOPS) mx0.op(Sn[0], m); else mx1.op(Sn[1], m - MaxQB::NOPS);
-            }
-#pragma unroll
-            for (int part = 32 * slot / NS; part < 32 * (slot + 1) / NS; ++part) sm.part(Sn[0], Pn0, part);
-            // DMA: spread over the phase
-            constexpr int ND = C::KP + C::VP;
-            if (slot % (NS / ND) == 1 && slot / (NS / ND) < ND) {
-                const int it = slot / (NS / ND);
-                if (it < C::KP) dma_k1(kds, ksl0, jk2, it);
-                else dma_v1(vds, vsl ^ 1, jv2, it - C::KP);
-            }
-            // the next block's Q piece j; past the last piece the DMA goes to this wave's
-            // O staging image (idle during the loop) from offset 0: no branch in the phase
-            if (slot == NS - 2) {
-                const bool qv = j < C::QP;
-                dma_q1(p4_desc(qpn, qv ? qnn : 0u), qbn, qv ? j : 0, qv ? qdst(j) : lds0 + C::OOFF + (uint32_t)wave * C::OST);
-            }
-        });
-        m_true[0] = vmax(m_true[0], mx0.mt);
-        m_true[1] = vmax(m_true[1], mx1.mt);
-        const bool f0 = __builtin_amdgcn_ballot_w64(mx0.mt > m_used[0] + thr_raw) != 0;
-        const bool f1 = __builtin_amdgcn_ballot_w64(mx1.mt > m_used[1] + thr_raw) != 0;
-        float ps0 = sm.sum();
-        FA_P4_STAMP(2);
-        if (f0 || f1) {   // rare: the running max moved by more than the threshold
-            p4_mfma_drain();
-            if (f0) {
-                const float mn = fmaxf(m_used[0], swap_halves_max(mx0.mt));
-                const float al = exp2_fast((m_used[0] - mn) * c);
-                l_run[0] *= al;
-#pragma unroll
-                for (int cb = 0; cb < C::NCB; ++cb)
-#pragma unroll
-                    for (int x = 0; x < 16; ++x) oacc[0][cb][x] *= al;
-                m_used[0] = mn;
-                ps0 = softmax_p(Sn[0], mn, Pn0);
-            }
-            if (f1) {
-                const float mn = fmaxf(m_used[1], swap_halves_max(mx1.mt));
-                const float al = exp2_fast((m_used[1] - mn) * c);
-                l_run[1] *= al;
-#pragma unroll
-                for (int cb = 0; cb < C::NCB; ++cb)
-#pragma unroll
-                    for (int x = 0; x < 16; ++x) oacc[1][cb][x] *= al;
-                m_used[1] = mn;
-            }
+        FA_P4_STAMP(3, j);
+        if constexpr (!LAST) {   // ---- Y: block 1 MFMAs ∥ block 0 softmax (tile j+1) ----
+            MaxQB mx;
+            SoftmaxQB<T> sm;
+            sm.c = c;
+            auto side = softmax_side(NMt{}, NPt{}, 0, mx, sm);
+            auto valu = [&](int i) __attribute__((always_inline)) {
+                side(i);
+                if (i >= NPRE && i < NPRE + C::KP) dma_k1(kds, ks0, jk2, i - NPRE);
+            };
+            auto mid = [&]() __attribute__((always_inline)) {
+                decide(0, mx.mt);
+                sm.nmc = -m_used[0] * c;
+            };
+            phase(Yes{}, Yes{}, NPt{}, 1, kslot, vslot, valu, mid);
+            l_run[0] += sm.sum();
+        } else {                 // ---- last tile: block 1's PV only; K(j+3) still goes out ----
+            auto valu = [&](int i) __attribute__((always_inline)) {
+                if (i < C::KP) dma_k1(kds, ks0, jk2, i);
+            };
+            phase(No{}, Yes{}, std::integral_constant<int, 1000>{}, 1, kslot, vslot, valu, nomid);
         }
-        l_run[0] += ps0;
+        FA_P4_STAMP(5, j);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::KP) : "memory");
+        FA_P4_STAMP(6, j);
     };
 
     // ---- prologue: the first block's Q and the first K / V tiles ----
@@ -463,12 +492,13 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         for (int it = 0; it < C::VP; ++it) dma_v1(vd0, 0, 0, it);
         p4_wait_all_barrier();
     }
-    FA_P4_STAMP(0);
+    FA_P4_STAMP(0, -1);
 
     int ks = 0, vs = 0;   // ring slots of this block's tile 0
     for (int k = 0;; ++k) {
         const int id = w + k * G;
         if (id >= nblk) break;
+        p4_blk = k;
         const int b = id / nqb, qb = id - b * nqb;
         const bool more = id + G < nblk;
         kp0 = kbase_of(id);
@@ -490,70 +520,49 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
                 const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(qimg + p4_qpos(16 * s + 8 * h + 4 + qq, tb)));
                 qf[u][s] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
             }
-        // S(0) (the pipeline restarts at each block)
-        phaseA(sA, kring + ks * C::KSLOT, no_valu);
-        p4_mfma_drain();
-        {
-            MaxQB m0, m1;
-#pragma unroll
-            for (int m = 0; m < MaxQB::NOPS; ++m) { m0.op(sA[0], m); m1.op(sA[1], m); }
-            m_true[0] = m0.mt;
-            m_true[1] = m1.mt;
-        }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            m_used[u] = swap_halves_max(m_true[u]);
+            m_used[u] = kNegInf;
+            m_true[u] = kNegInf;
+            l_run[u] = 0.0f;
 #pragma unroll
             for (int cb = 0; cb < C::NCB; ++cb)
 #pragma unroll
                 for (int x = 0; x < 16; ++x) oacc[u][cb][x] = 0.0f;
         }
-        l_run[0] = softmax_p(sA[0], m_used[0], pA0);
-        l_run[1] = 0.0f;
-        FA_P4_STAMP(1);
+        // S(0) of both query blocks (the pipeline restarts at each block)
+        phase(Yes{}, No{}, std::integral_constant<int, 1000>{}, 0, kring + ks * C::KSLOT, nullptr, none, nomid);
+        phase(Yes{}, No{}, std::integral_constant<int, 1000>{}, 1, kring + ks * C::KSLOT, nullptr, none, nomid);
+        // every wave's K(0) and Q reads are done before any wave DMAs into those places
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+        {   // block 0's tile-0 softmax (not overlapped)
+            MaxQB mx;
+#pragma unroll
+            for (int m = 0; m < MaxQB::NOPS; ++m) mx.op(S[0], m);
+            decide(0, mx.mt);
+            SoftmaxQB<T> sm;
+            sm.c = c;
+            sm.nmc = -m_used[0] * c;
+#pragma unroll
+            for (int part = 0; part < 32; ++part) sm.part(S[0], P[0], part);
+            l_run[0] += sm.sum();
+        }
+        FA_P4_STAMP(1, -1);
 
-        // tiles 0 .. NT-2 in pairs (the S / P buffers alternate), then the last tile
-        int j = 0;
-        int k0 = ks, k1 = ks == 2 ? 0 : ks + 1, v0 = vs;
-        auto adv = [&]() {
+        int k1 = ks == 2 ? 0 : ks + 1, k0 = ks, v0 = vs;   // slots of K(j+1), K(j), V(j)
+        for (int j = 0; j < NT - 1; ++j) {
+            tile(No{}, j, k1, k0, v0);
             k0 = k1;
             k1 = k1 == 2 ? 0 : k1 + 1;
             v0 ^= 1;
-        };
-        bool lastB = false;
-        for (;;) {
-            if (j + 1 >= NT) break;
-            step(j, k0, k1, v0, sA, sB, pA0, pB0);
-            ++j;
-            adv();
-            if (j + 1 >= NT) { lastB = true; break; }
-            step(j, k0, k1, v0, sB, sA, pB0, pA0);
-            ++j;
-            adv();
         }
-        // ---- last tile j = NT-1 (in sB / pB0 when lastB) ----
-        auto last = [&](f32x16 (&Sc)[2][2], F8 (&Pc0)[2][2]) {
-            l_run[1] += softmax_p(Sc[1], m_used[1], p1);
-            p4_wait_all_barrier();
-            const int jk = j + 3 - NT, jv = j + 1 - NT;   // both in the next block
-            phaseB(vring + v0 * C::VSLOT, Pc0, p1, [&](int slot) {
-                constexpr int ND = C::KP + C::VP;
-                constexpr int NS = 2 * C::NVQ;
-                if (slot % (NS / ND) == 1 && slot / (NS / ND) < ND) {
-                    const int it = slot / (NS / ND);
-                    if (it < C::KP) dma_k1(p4_desc(kp1, kn1), k0, jk, it);
-                    else dma_v1(p4_desc(vp1, vn1), v0 ^ 1, jv, it - C::KP);
-                }
-            });
-        };
-        if (lastB) last(sB, pB0); else last(sA, pA0);
+        tile(Yes{}, NT - 1, k1, k0, v0);
         // next block's ring slots: tile NT of this stream
         ks = k1;
         vs = v0 ^ 1;
-        FA_P4_STAMP(3);
+        FA_P4_STAMP(7, -1);
 
         // ---- epilogue: O / l through the wave's staging image, l and m ----
-        p4_mfma_drain();
         const auto ors = slab_rsrc((T*)p.O + (int64_t)b * N * dv, (uint32_t)(N * dv * (int)sizeof(T)));
         float inv[2];
 #pragma unroll
@@ -586,7 +595,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
                 __builtin_amdgcn_raw_buffer_store_b128(v4, ors, off, 0, 0);
             }
         }
-        FA_P4_STAMP(4);
+        FA_P4_STAMP(8, -1);
     }
 }
 
