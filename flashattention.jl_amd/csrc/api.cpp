@@ -100,16 +100,20 @@ int fa_abi_version(void) { return FA_HIP_ABI_VERSION; }
 int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
 
 // Not part of the public header: selects the forward kernel variant for A/B
-// benchmarking: 0 = auto (per head-dim class), 4..7 = {waves, query blocks per
-// wave} = {4,1}, {8,1}, {4,2}, {8,2} on 32x32x16 MFMA; 8, 9 = 8 waves x
-// {64, 32} query rows on 16x16x32 MFMA; 16 = 8 waves x 32 rows at 4 waves per SIMD;
-// 20 = the default geometries with per-element Q gathers and O stores; 30 = the
-// one-wave-per-SIMD persistent kernel (fa_fwd_p4.hip) where its shape rules allow.
+// benchmarking: 0 = auto (per head-dim class), 5 / 7 = 8 waves x {1, 2} query
+// blocks per wave on 32x32x16 MFMA; 20 = the default geometries with per-element Q
+// gathers and O stores; 30 = the one-wave-per-SIMD persistent kernel (fa_fwd_p4.hip)
+// where its shape rules allow.  (The measured-and-rejected 4-wave, 16x16x32 and
+// 4-waves-per-SIMD geometries were removed in round 4; git history keeps them.)
 int fa_debug_set_fwd_variant(int v) {
     const int old = fa::g_fwd_variant;
-    if (v == 0 || (v >= 4 && v <= 9) || v == 16 || v == 20 || v == 30) fa::g_fwd_variant = v;
+    if (v == 0 || v == 5 || v == 7 || v == 20 || v == 30) fa::g_fwd_variant = v;
     return old;
 }
+
+// Not part of the public header: 30 when the calling thread's last bf16/f16 fast-path
+// forward ran the one-wave-per-SIMD kernel (fa_fwd_p4.hip), 0 otherwise (tests).
+int fa_debug_fwd_last_path(void) { return fa::g_fwd_last_path; }
 
 // Not part of the public header: lazy-rescale threshold of the bf16/f16 forward
 // kernels in log2 units (default 8; 0 = rescale on every max increase, the
@@ -157,11 +161,11 @@ int fa_debug_set_circ_generic(int v) {
 // Not part of the public header: windowed forward path override (1 composed,
 // 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window
 // row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the auto choice at ws <= 7),
-// 7 / 8 two- / four-window LDS-DMA with rotated slots, 9 segment-owning (16-B y stores),
-// 10 eight-window strip (stride == ws), where eligible; 0 auto).
+// 10 eight-window strip (stride == ws), where eligible; 0 auto).  Modes 7-9 (rejected
+// experimental kernels) were removed; they now select the auto path.
 int fa_debug_set_win_composed(int v) {
     const int old = fa::g_win_force_composed;
-    fa::g_win_force_composed = (v >= 1 && v <= 10) ? v : 0;
+    fa::g_win_force_composed = ((v >= 1 && v <= 6) || v == 10) ? v : 0;
     return old;
 }
 

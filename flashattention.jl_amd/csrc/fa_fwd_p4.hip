@@ -45,6 +45,12 @@
 #ifndef FA_P4_STAMP
 #define FA_P4_STAMP(pt, j)
 #endif
+// FA_P4_ABL: timing-only ablations of the diagnostic build (WRONG results): 1 no K/V/Q
+// DMA in the tile loop, 2 no exponentials, 4 no LDS operand reads in the tile loop,
+// 8 no softmax / max VALU work at all.
+#ifndef FA_P4_ABL
+#define FA_P4_ABL 0
+#endif
 
 namespace fa {
 
@@ -140,15 +146,14 @@ __device__ __forceinline__ int p4_qpos(int f, int lb) {
 // Hazards inside the hot loop are the kernel's: an exponential's consumer is never the
 // next instruction (part1 of chunk c follows part0 of chunk c+1), and the scores an
 // asm MFMA writes are read a phase later.
-template <class T> struct P4Cvt;
-template <> struct P4Cvt<bf16> { static constexpr const char* op = "v_cvt_pk_bf16_f32"; };
-template <> struct P4Cvt<f16> { static constexpr const char* op = "v_cvt_pk_f16_f32"; };
-
 __device__ __forceinline__ void p4_exp2x2(float& e0, float& e1, float s0, float s1, float c, float nmc) {
     float t0, t1;
-    asm volatile("v_fma_f32 %2, %4, %6, %7\n\tv_fma_f32 %3, %5, %6, %7\n\tv_exp_f32 %0, %2\n\tv_exp_f32 %1, %3"
-                 : "=&v"(e0), "=&v"(e1), "=&v"(t0), "=&v"(t1)
-                 : "v"(s0), "v"(s1), "s"(c), "v"(nmc));
+    if (FA_P4_ABL & 2)
+        asm volatile("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %5" : "=&v"(e0), "=&v"(e1) : "v"(s0), "v"(s1), "s"(c), "v"(nmc));
+    else
+        asm volatile("v_fma_f32 %2, %4, %6, %7\n\tv_fma_f32 %3, %5, %6, %7\n\tv_exp_f32 %0, %2\n\tv_exp_f32 %1, %3"
+                     : "=&v"(e0), "=&v"(e1), "=&v"(t0), "=&v"(t1)
+                     : "v"(s0), "v"(s1), "s"(c), "v"(nmc));
 }
 template <class T>
 __device__ __forceinline__ unsigned p4_pack(float e0, float e1) {
@@ -320,6 +325,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         asm volatile("" : "+v"(ko[0]), "+v"(ko[1]), "+v"(vo[0][0]), "+v"(vo[0][1]), "+v"(vo[1][0]), "+v"(vo[1][1]));
         F8 fr[3];
         auto rd = [&](int i) __attribute__((always_inline)) {
+            if ((FA_P4_ABL & 4) && i >= 2 && (PV || QK) && NM > 8) return;
             if (i < NKQ) {
                 const int kb = i / C::NKS, s = i % C::NKS;
                 const char* a = kslot + ko[kb] + 16 * s * 128;
@@ -362,6 +368,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
     // previous phase, l_v and O_v are scaled together.  m_used starts at −inf, so the
     // first tile always takes the branch (scaling O = 0, l = 0 by 0).
     auto decide = [&](int v, float mt) __attribute__((always_inline)) {
+        if (FA_P4_ABL & 8) mt = 0.0f;
         m_true[v] = vmax(m_true[v], mt);
         if (__builtin_amdgcn_ballot_w64(mt > m_used[v] + thr_raw) != 0) {
             const float mn = fmaxf(m_used[v], swap_halves_max(mt));
@@ -381,6 +388,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
     auto softmax_side = [&](auto NMt, auto NPREt, int v, MaxQB& mx, SoftmaxQB<T>& sm) __attribute__((always_inline)) {
         constexpr int NM = decltype(NMt)::value, NPRE = decltype(NPREt)::value;
         return [&, v](int i) __attribute__((always_inline)) {
+            if (FA_P4_ABL & 8) return;
             if (i < NPRE) {
 #pragma unroll
                 for (int m = MaxQB::NOPS * i / NPRE; m < MaxQB::NOPS * (i + 1) / NPRE; ++m) mx.op(S[v], m);
@@ -432,6 +440,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
                 // V(j+1) pieces and the Q piece early in the phase
                 constexpr int NMx = LAST ? C::NVQ : NMF;
                 constexpr int NPx = LAST ? (C::NVQ >= 16 ? 4 : 2) : NPRE;
+                if (FA_P4_ABL & 1) return;
                 if (i >= NPx && i < NPx + C::VP) dma_v1(vds, vs0 ^ 1, jv2, i - NPx);
                 if (i == NPx + C::VP) {
                     const bool qv = j < C::QP;
@@ -454,7 +463,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
             auto side = softmax_side(NMt{}, NPt{}, 0, mx, sm);
             auto valu = [&](int i) __attribute__((always_inline)) {
                 side(i);
-                if (i >= NPRE && i < NPRE + C::KP) dma_k1(kds, ks0, jk2, i - NPRE);
+                if (!(FA_P4_ABL & 1) && i >= NPRE && i < NPRE + C::KP) dma_k1(kds, ks0, jk2, i - NPRE);
             };
             auto mid = [&]() __attribute__((always_inline)) {
                 decide(0, mx.mt);
@@ -464,7 +473,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
             l_run[0] += sm.sum();
         } else {                 // ---- last tile: block 1's PV only; K(j+3) still goes out ----
             auto valu = [&](int i) __attribute__((always_inline)) {
-                if (i < C::KP) dma_k1(kds, ks0, jk2, i);
+                if (!(FA_P4_ABL & 1) && i < C::KP) dma_k1(kds, ks0, jk2, i);
             };
             phase(No{}, Yes{}, std::integral_constant<int, 1000>{}, 1, kslot, vslot, valu, nomid);
         }

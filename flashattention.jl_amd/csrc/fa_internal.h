@@ -140,6 +140,7 @@ constexpr int kMaxHeadDim = 128;
 // the kernels that thread launches, so concurrent callers on other threads stay
 // on the default paths and the public entry points remain stateless for them.
 extern thread_local int g_fwd_variant;        // forward kernel variant
+extern thread_local int g_fwd_last_path;      // 30 when the last fast forward launch ran fa_fwd_p4
 extern thread_local float g_fwd_rescale_log2; // forward fast kernels: lazy-rescale threshold (log2 units)
 extern thread_local int g_bwd_force_generic;  // backward: force the generic SIMT path
 extern thread_local int g_bwd_mode;           // backward MFMA path: 0 auto, 1 split passes, 2 single pass

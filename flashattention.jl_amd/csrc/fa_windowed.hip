@@ -979,256 +979,6 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
 }
 
 // --------------------------------------------------------------------------
-// NW (2 or 4) horizontally adjacent windows per workgroup staged by LDS-DMA
-// (bf16/f16, 2-D, stride >= ws, ws <= 7, d, dv <= 64, width % 8 == 0, 16-B
-// aligned).  An experimental LDS-DMA variant, NOT the default (the default is
-// win_rows1s<..., 2>): the dispatcher launches it only under debug modes 7 / 8 of
-// fa_debug_set_win_composed, and it measured no faster.
-//
-// Slots are ROTATED instead of shifted: slot (yy, sx) of window w holds pixel
-// (ax + sx, y0 + yy) with ax = clamp(xs & ~1, 0, W - 8) the dword-aligned start
-// of the 16-B row load, so a (feature, window row) item is one 16-B buffer load
-// straight into LDS (buffer_load ... lds): no registers, shifts or ds_write.
-// Keys outside the window (the neighbours' pixels in the slot row, slot rows
-// >= ws) are masked; rows outside the image load as 0 (zero-padding tokens,
-// unmasked as in the reference); padding COLUMNS have no slot and are added to
-// the softmax analytically (npad zero keys: score 0, value 0), and their own
-// query tokens (q = 0: every score 0) get m = 0, l = T.
-//
-// LDS: per tensor an image [feature][NW windows][8 chunks of 8 slots]
-// (NW·128-B feature rows), so one DMA instruction (1 KiB) carries all NW
-// windows' rows of 1024 / (NW·128) features: the windows share cache lines and
-// the L1 -> L2 requests per byte fall with NW (the texture path, not HBM, bounds
-// this kernel: TA busy ~70 %, 8.7 M read requests per configs[2] B=32 call at
-// NW = 2).  16-B chunk XOR swizzles, conflict-free for the reads that use them:
-//   Q, K  (ds_read_b64_tr_b16, rows f..f+3 x 64 B): window ^ (f & 1), chunk ^ ((f >> 1) & 1) << 2;
-//   V     (ds_read_b128 rows, 16 features per lane group): window ^ ((f >> 3) & 1), chunk ^ (f & 7).
-// At NW = 4 the V image reuses the Q image (its DMA is issued once every wave
-// has finished QKᵀ and lands under the softmax), so two workgroups fit per CU.
-// --------------------------------------------------------------------------
-template <int NW>
-__device__ __forceinline__ int qk_slot(int f, int w, int c) {
-    return f * (NW * 128) + ((w ^ (f & 1)) << 7) + ((c ^ (((f >> 1) & 1) << 2)) << 4);
-}
-template <int NW>
-__device__ __forceinline__ int v_slot(int f, int w, int c) {
-    return f * (NW * 128) + ((w ^ ((f >> 3) & 1)) << 7) + ((c ^ (f & 7)) << 4);
-}
-
-template <class T, int D, int DV, int NW>
-__global__ __launch_bounds__(256 * NW, 8) void win_dma(const T* __restrict__ q, const T* __restrict__ k,
-                                                    const T* __restrict__ v, T* __restrict__ out,
-                                                    float* __restrict__ lo, float* __restrict__ mo, WinDev g, int d,
-                                                    int dv, int nwin_total, float scale, float scale_log2) {
-    typedef typename Frag8<T>::type F8;
-    typedef typename Frag8<T>::half F4;
-    static_assert(NW == 2 || NW == 4, "windows per workgroup");
-    constexpr int ROW = NW * 128, NWAVE = 4 * NW;
-    constexpr bool ALIAS = DV <= D;                     // V over the Q image
-    constexpr int QIMG = D * ROW, VIMG = DV * ROW, VOFF = ALIAS ? 0 : 2 * QIMG;
-    constexpr int LDSB = (VOFF + VIMG > 2 * QIMG) ? VOFF + VIMG : 2 * QIMG;
-    constexpr int FPB = 1024 / ROW;                     // features per 1-KiB DMA block
-    constexpr int NBQ = D / FPB, NBV = DV / FPB;
-    constexpr int NQK = 2 * NBQ / NWAVE, NV = NBV / NWAVE;   // DMA instructions per wave
-    static_assert(2 * NBQ % NWAVE == 0 && NBV % NWAVE == 0, "DMA split");
-    __shared__ __attribute__((aligned(16))) char smem[LDSB];
-
-    FA_STAMP(0);
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
-    const int wid0 = xcd_remap(blockIdx.x, gridDim.x) * NW;
-    const int nperimg = g.O[0] * g.O[1];
-    struct Win { int wx, wy, b, xs, y0, ax; bool ok; };
-    auto win_at = [&](int wl) {
-        Win w;
-        const int id = wid0 + wl;
-        w.ok = id < nwin_total;
-        const int idc = w.ok ? id : 0;
-        w.b = idc / nperimg;
-        const int rem = idc - w.b * nperimg;
-        w.wy = rem / g.O[0];
-        w.wx = rem - w.wy * g.O[0];
-        w.xs = w.wx * st - g.pad;
-        w.y0 = w.wy * st - g.pad;
-        w.ax = min(max(w.xs & ~1, 0), W_ - 8);
-        return w;
-    };
-    // named values, not an array: selecting among array elements by a lane value
-    // made the compiler index a scratch copy
-    const Win wn0 = win_at(0), wn1 = win_at(1), wn2 = NW > 2 ? win_at(2) : wn0, wn3 = NW > 2 ? win_at(3) : wn0;
-    auto sel = [](int x, int a0, int a1, int a2, int a3) { return x == 0 ? a0 : x == 1 ? a1 : x == 2 ? a2 : a3; };
-    auto pick = [&](int x) -> Win {   // field by field (a struct select went through scratch too)
-        Win w;
-        w.wx = sel(x, wn0.wx, wn1.wx, wn2.wx, wn3.wx);
-        w.wy = sel(x, wn0.wy, wn1.wy, wn2.wy, wn3.wy);
-        w.b = sel(x, wn0.b, wn1.b, wn2.b, wn3.b);
-        w.xs = sel(x, wn0.xs, wn1.xs, wn2.xs, wn3.xs);
-        w.y0 = sel(x, wn0.y0, wn1.y0, wn2.y0, wn3.y0);
-        w.ax = sel(x, wn0.ax, wn1.ax, wn2.ax, wn3.ax);
-        w.ok = sel(x, wn0.ok, wn1.ok, wn2.ok, wn3.ok) != 0;
-        return w;
-    };
-    const int b0 = wn0.b;
-    const int nimg = min(2, nwin_total / nperimg - b0);   // a window group may straddle two images
-    const auto qrs = slab_rsrc(q + (int64_t)b0 * d * P_, (uint32_t)(nimg * d * P_ * 2));
-    const auto krs = slab_rsrc(k + (int64_t)b0 * d * P_, (uint32_t)(nimg * d * P_ * 2));
-    const auto vrs = slab_rsrc(v + (int64_t)b0 * dv * P_, (uint32_t)(nimg * dv * P_ * 2));
-
-    // ---- DMA: lane -> (feature, window slot, chunk) of a 1-KiB block ----
-    auto dma = [&](__amdgpu_buffer_rsrc_t rs, char* img, int blk, int C, bool vlay) {
-        const int f = blk * FPB + lane / (ROW / 16), wp = (lane >> 3) & (NW - 1), pc = lane & 7;
-        const int wsel = vlay ? wp ^ ((f >> 3) & 1) : wp ^ (f & 1);
-        const int yy = vlay ? pc ^ (f & 7) : pc ^ (((f >> 1) & 1) << 2);
-        const Win ww = pick(wsel);
-        const int wb = ww.b, wy0 = ww.y0, wax = ww.ax;
-        const bool wok = ww.ok;
-        const int y = wy0 + yy;
-        const bool ok = wok && yy < ws && y >= 0 && y < H_ && f < C;
-        const int off = ok ? (((wb - b0) * C + f) * P_ + y * W_ + wax) * 2 : 0x7FFFFFF0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16,
-                                                 (FA_WIN_ABL & 2) ? 0 : off, 0, 0, 0);
-    };
-#pragma unroll
-    for (int i = 0; i < NQK; ++i) {
-        const int gb = i * NWAVE + wave;                 // Q blocks then K blocks
-        if (gb < NBQ) dma(qrs, smem, gb, d, false);
-        else dma(krs, smem + QIMG, gb - NBQ, d, false);
-    }
-    if constexpr (!ALIAS) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) dma(vrs, smem + VOFF, i * NWAVE + wave, dv, true);
-        // Q, K landed (this wave's: vmcnt counts the NV later V blocks), then everyone's
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    FA_STAMP(2);
-
-    // ---- this wave's window, query block and v chunk ----
-    const int wl = wave >> 2;
-    const Win w = pick(wl);
-    const int qb = wave & 1, vc = (wave >> 1) & 1;
-    const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-    // window columns in slot coordinates: slot sx is a real key iff c0 <= sx < c1
-    const int c0 = w.xs - w.ax, c1 = c0 + ws;
-    const int ncols = min(c1, 8) - max(c0, 0);
-    const float npad = (float)((ws - ncols) * ws);       // padding-column tokens (zero keys)
-    f32x16 sa[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int x = 0; x < 16; ++x) sa[kb][x] = 0.0f;
-    // tr-read offsets: feature rows 16·s16 + 8h + qq (+4); the swizzle depends on qq only
-    const int kro = qk_slot<NW>(8 * h + qq, wl, kh * 2 + (sig >> 1)) + (sig & 1) * 8;
-    const int qro = qk_slot<NW>(8 * h + qq, wl, qb * 4 + kh * 2 + (pp >> 1)) + (pp & 1) * 8;
-#pragma unroll
-    for (int s16 = 0; s16 < D / 16; ++s16) {
-        F8 kf[2];
-#pragma unroll
-        for (int blk = 0; blk < 2; ++blk) {
-            // key block blk = chunk bit 2, which the swizzle XORs: flip byte-offset bit 6
-            const char* a = smem + QIMG + ((kro + s16 * 16 * ROW) ^ (blk << 6));
-            kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
-                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * ROW)), 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-        const char* a = smem + qro + s16 * 16 * ROW;
-        const F8 qf = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
-                                              __builtin_bit_cast(F4, ds_read_tr16(a + 4 * ROW)), 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) sa[kb] = mfma32x32x16(kf[kb], qf, sa[kb]);
-    }
-    FA_STAMP(3);
-    if constexpr (ALIAS) {
-        // every wave is done with the Q image: V over it, landing under the softmax
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < NV; ++i) dma(vrs, smem + VOFF, i * NWAVE + wave, dv, true);
-    }
-
-    // ---- exact softmax per query over the window's real keys (+ npad zero keys) ----
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-            const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
-            const int sx = kt & 7;
-            if ((kt >> 3) >= ws || sx < c0 || sx >= c1) sa[kb][x] = kNegInf;
-        }
-    float mt = swap_halves_max(lane_max<2>(sa));
-    if (npad > 0.0f) mt = vmax(mt, 0.0f);
-    const float mc = mt * scale_log2;
-    float ps[4];
-    F8 pf[2][2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-            const float pr = exp2_fast(fmaf(sa[kb][x], scale_log2, -mc));
-            if (kb == 0 && x < 4) ps[x] = pr; else ps[x & 3] += pr;
-            pf[kb][x >> 3][x & 7] = (T)pr;
-        }
-    float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
-    if (npad > 0.0f) lt = fmaf(npad, exp2_fast(-mc), lt);
-    FA_STAMP(4);
-
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                                     // V landed
-
-    // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
-    unsigned vm[4];                                      // key-slot mask of a V fragment (one slot row)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        vm[j] = ((2 * j >= c0 && 2 * j < c1) ? 0x0000FFFFu : 0u) | ((2 * j + 1 >= c0 && 2 * j + 1 < c1) ? 0xFFFF0000u : 0u);
-    const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
-#pragma unroll
-    for (int cv = vc; cv < DV / 32 && w.ok; cv += 2) {
-        const int f = cv * 32 + r;
-        f32x16 oa;
-#pragma unroll
-        for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                u32x4 vr = *(const u32x4*)(smem + VOFF + v_slot<NW>(f, wl, kb * 4 + s2 * 2 + h));
-#pragma unroll
-                for (int j = 0; j < 4; ++j) vr[j] &= vm[j];
-                oa = mfma32x32x16(__builtin_bit_cast(F8, vr), pf[kb][s2], oa);
-            }
-        const int px = w.ax + qtx, py = w.y0 + qty;
-        if (qtx >= c0 && qtx < c1 && qty < ws && py >= 0 && py < H_) {
-            const float inv = 1.0f / lt;
-            T* yb = out + (int64_t)w.b * dv * P_ + (int64_t)py * W_ + px;
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int cc = cv * 32 + acc_row(x, h);
-                if (cc < dv && (!(FA_WIN_ABL & 1) || oa[x] == 1234.5f)) yb[(int64_t)cc * P_] = (T)(oa[x] * inv);
-            }
-        }
-    }
-    if (w.ok && vc == 0) {
-        const int64_t wbase = (int64_t)g.T * ((int64_t)(w.wx + g.O[0] * w.wy) + (int64_t)g.L * w.b);
-        if (h == 0 && qtx >= c0 && qtx < c1 && qty < ws) {
-            const int64_t li = wbase + qty * ws + (qtx - c0);
-            mo[li] = mt * scale;
-            lo[li] = lt;
-        }
-        // padding-column query tokens (q = 0): every score is 0
-        if (qb == 0 && lane < g.T) {
-            const int px = w.xs + lane % ws;
-            if (px < 0 || px >= W_) {
-                mo[wbase + lane] = 0.0f;
-                lo[wbase + lane] = (float)g.T;
-            }
-        }
-    }
-    FA_STAMP(5);
-}
-
-// --------------------------------------------------------------------------
 // Strip kernel: NS = 8 horizontally adjacent windows of one window row per
 // workgroup, one window per wave (bf16/f16, 2-D, stride == ws <= 7, d, dv <= 64,
 // width % 8 == 0, q, k, v, y 16-B aligned; the default for large launches).
@@ -1254,7 +1004,7 @@ __global__ __launch_bounds__(256 * NW, 8) void win_dma(const T* __restrict__ q, 
 //   * y: per V chunk, each wave writes its window's normalised O into a strip
 //     image [32 f][8 rows][64 px] over that V chunk, then the workgroup stores it
 //     row by row.
-// Slots are ROTATED as in win_dma: slot (yy, sx) of window w holds pixel
+// Slots are ROTATED: slot (yy, sx) of window w holds pixel
 // (ax_w + sx, y0 + yy), ax_w = clamp(xs_w & ~1, 0, W - 8); padding columns enter
 // the softmax analytically (npad zero keys), padding rows load as zeros.
 // LDS-DMA writes lane-linearly, so the swizzles are applied through each lane's
@@ -1536,235 +1286,6 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
         if (vc == 0) FA_STAMP(4);
     }
     FA_STAMP(5);
-}
-
-// --------------------------------------------------------------------------
-// Segment-owning windowed forward (bf16/f16, 2-D, stride >= ws, ws <= 7,
-// d, dv <= 64, width % 32 == 0, 16-B aligned q, k, v, y; mode 9, §2.3).
-//
-// The y stores of the per-window kernels are 2-B writes to 128-B lines that
-// ≈ 9 windows of different workgroups share: 49 µs of the 80-µs configs[2]
-// B = 32 forward on their own, against 11 µs for 16-B stores of lines (or 64-B
-// half lines) that one workgroup owns (tools/exp/store_pattern.hip).  So a
-// workgroup here owns a 32-pixel segment of one window row's image rows: it
-// computes every window that meets the segment (the two boundary windows also
-// by the neighbour: ≈ 10 % more windows), two at a time with the row-shift
-// staging of win_rows1s and the next pair's rows prefetched into registers,
-// keeps O of the segment's pixels in LDS, and stores it as 16-B chunks.
-// Pixels no window covers stay NaN (the staging starts as NaN).  V is staged
-// over the window's Q|K images once every wave has finished QKᵀ, so LDS is
-// 2·(2·D·128) + 8·dv·64 bytes (64 KB at 64 / 64): two workgroups per CU.
-// --------------------------------------------------------------------------
-template <class T, int D, int DV>
-__global__ __launch_bounds__(512, 4) void win_seg(const T* __restrict__ q, const T* __restrict__ k,
-                                                  const T* __restrict__ v, T* __restrict__ out,
-                                                  float* __restrict__ lo, float* __restrict__ mo, WinDev g, int d,
-                                                  int dv, float scale, float scale_log2) {
-    typedef typename Frag8<T>::type F8;
-    typedef typename Frag8<T>::half F4;
-    constexpr int NTH = 512, KROW = 128, SEGW = 32;
-    constexpr int QIMG = D * KROW, REGION = 2 * QIMG;           // Q | K of one window; V over both
-    static_assert(DV * 128 <= REGION, "V image over Q|K");
-    constexpr int OST = DV * 8 * SEGW * 2;                      // O of the segment: [feature][8 rows][32 px]
-    constexpr int NIQ = D * 8 / 256, NIV = DV * 8 / 256;        // row items per thread (2 windows)
-    static_assert(D * 8 % 256 == 0 && DV * 8 % 256 == 0, "item split");
-    __shared__ __attribute__((aligned(16))) char smem[2 * REGION + OST];
-    char* const ost = smem + 2 * REGION;
-    auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride, pad = g.pad;
-    const int nsr = W_ / SEGW;                                  // segments per image row
-    const int sid = xcd_remap(blockIdx.x, gridDim.x);
-    const int b = sid / (g.O[1] * nsr), rem = sid - b * (g.O[1] * nsr);
-    const int wy = rem / nsr, x0 = (rem - wy * nsr) * SEGW, y0 = wy * st - pad;
-    // windows that meet [x0, x0 + 32): wx·st − pad + ws > x0 and wx·st − pad < x0 + 32
-    const int num = x0 + pad - ws;
-    const int wlo = num < 0 ? 0 : num / st + 1;
-    const int whi = min((x0 + SEGW + pad + st - 1) / st - 1, g.O[0] - 1);
-    const int np = whi >= wlo ? (whi - wlo + 2) / 2 : 0;        // window pairs
-    struct Win { int xs, ax; bool ok; };
-    auto win_of = [&](int p, int wl) {
-        Win w;
-        const int wx = wlo + 2 * p + wl;
-        w.ok = wx <= whi;
-        w.xs = (w.ok ? wx : wlo) * st - pad;
-        w.ax = min(max(w.xs & ~1, 0), W_ - 8);
-        return w;
-    };
-    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
-    // item it -> (window it & 1, feature (it >> 1) >> 3, slot row (it >> 1) & 7)
-    auto item_off = [&](int p, int it, int C) {
-        const Win w = win_of(p, it & 1);
-        const int rest = it >> 1, yy = rest & 7, f = rest >> 3, y = y0 + yy;
-        const bool ok = w.ok && yy < ws && y >= 0 && y < H_ && f < C;
-        return ok ? (f * P_ + y * W_ + w.ax) * 2 : 0x7FFFFFF0;
-    };
-    u32x4 rq[NIQ], rk[NIQ], rv[NIV];
-    auto load_pair = [&](int p, u32x4 (&aq)[NIQ], u32x4 (&ak)[NIQ], u32x4 (&av)[NIV]) {
-#pragma unroll
-        for (int j = 0; j < NIQ; ++j) {
-            const int o = item_off(p, tid + NTH * j, d);
-            aq[j] = __builtin_amdgcn_raw_buffer_load_b128(qrs, o, 0, 0);
-            ak[j] = __builtin_amdgcn_raw_buffer_load_b128(krs, o, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < NIV; ++j) av[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, item_off(p, tid + NTH * j, dv), 0, 0);
-    };
-    if (np > 0) load_pair(0, rq, rk, rv);
-    {   // O staging starts as NaN: pixels no window covers keep it (0/0 in the reference)
-        const unsigned short nb = __builtin_bit_cast(unsigned short, (T)__builtin_nanf(""));
-        const unsigned nn = nb | ((unsigned)nb << 16);
-        const u32x4 n4 = {nn, nn, nn, nn};
-#pragma unroll
-        for (int i = 0; i < OST / 16 / NTH; ++i) *(u32x4*)(ost + (tid + NTH * i) * 16) = n4;
-    }
-    // staging of one row item: shift into slots, mask (slot < ws, pixel inside the image);
-    // part 0 Q, 1 K (128-B rows, 32-B swizzle), 2 V (over Q|K, 128-B rows, 16-B swizzle)
-    auto stage = [&](int p, const u32x4& val, int it, int part) {
-        const int wl = it & 1;
-        const Win w = win_of(p, wl);
-        const int rest = it >> 1, yy = rest & 7, f = rest >> 3;
-        unsigned mask[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int t0 = 2 * j, t1 = 2 * j + 1;
-            const bool v0 = t0 < ws && w.xs + t0 >= 0 && w.xs + t0 < W_;
-            const bool v1 = t1 < ws && w.xs + t1 >= 0 && w.xs + t1 < W_;
-            mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
-        }
-        const u32x4 o = shift_row_lane(val, w.xs - w.ax, mask);
-        char* base = smem + wl * REGION;
-        const int off = part == 2 ? f * 128 + ((yy ^ ((f >> 1) & 7)) * 16)
-                                  : part * QIMG + f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
-        *(u32x4*)(base + off) = o;
-    };
-
-    const int wl = wave >> 2;
-    char* const wsm = smem + wl * REGION;
-    const int qb = wave & 1, vc = (wave >> 1) & 1;
-    for (int p = 0; p < np; ++p) {
-        // lane-dependent values re-derived every pair from an opaque copy of the lane id
-        // (hoisted out of the loop they spilled)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int r = ln & 31, h = ln >> 5;
-        const int g4 = ln >> 4, kh = g4 & 1, qq = (ln & 15) >> 2, pp = ln & 3;
-        const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
-        const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
-#pragma unroll
-        for (int j = 0; j < NIQ; ++j) {
-            stage(p, rq[j], tid + NTH * j, 0);
-            stage(p, rk[j], tid + NTH * j, 1);
-        }
-        u32x4 nq[NIQ], nk[NIQ], nv[NIV];
-        const bool more = p + 1 < np;
-        if (more) load_pair(p + 1, nq, nk, nv);   // the next pair's rows land under this one
-        lds_barrier();
-
-        // ---- Sᵀ = K Qᵀ for this wave's query block (keys of the window on rows) ----
-        f32x16 sa[2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) sa[kb][x] = 0.0f;
-#pragma unroll
-        for (int s16 = 0; s16 < D / 16; ++s16) {
-            const int orow = (16 * s16 + 8 * h + qq) * KROW;
-            F8 kf[2];
-#pragma unroll
-            for (int blk = 0; blk < 2; ++blk) {
-                const char* a = wsm + QIMG + orow + (((blk * 2 + kh) ^ kswz(qq)) * 32) + 8 * sig;
-                kf[blk] = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
-                                                  __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
-            }
-            const char* a = wsm + orow + (((qb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
-            const F8 qf = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
-                                                  __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb) sa[kb] = mfma32x32x16(kf[kb], qf, sa[kb]);
-        }
-        lds_barrier();                               // every wave is done with Q, K: V over them
-#pragma unroll
-        for (int j = 0; j < NIV; ++j) stage(p, rv[j], tid + NTH * j, 2);
-
-        // ---- exact softmax per query (keys: the window's ws x ws real slots) ----
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int kt = kb * 32 + (x & 3) + 4 * ((x >> 2) & 1) + 8 * h + 16 * (x >> 3);
-                if ((kt & 7) >= ws || (kt >> 3) >= ws) sa[kb][x] = kNegInf;
-            }
-        const float mt = swap_halves_max(lane_max<2>(sa));
-        const float mc = mt * scale_log2;
-        float ps[4];
-        F8 pf[2][2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const float pr = exp2_fast(fmaf(sa[kb][x], scale_log2, -mc));
-                if (kb == 0 && x < 4) ps[x] = pr; else ps[x & 3] += pr;
-                pf[kb][x >> 3][x & 7] = (T)pr;
-            }
-        const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
-        lds_barrier();                               // V staged
-
-        // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, into the segment's O staging ----
-        const Win w = win_of(p, wl);
-        const int px = w.xs + qtx;
-        const bool mine = w.ok && qtx < ws && qty < ws && px >= x0 && px < x0 + SEGW;
-#pragma unroll
-        for (int cv = vc; cv < DV / 32; cv += 2) {
-            const int f = cv * 32 + r;
-            f32x16 oa;
-#pragma unroll
-            for (int x = 0; x < 16; ++x) oa[x] = 0.0f;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
-                    oa = mfma32x32x16(*(const F8*)(wsm + f * 128 + ((((kb * 4 + 2 * s2 + h) ^ ((f >> 1) & 7))) * 16)),
-                                      pf[kb][s2], oa);
-            if (mine) {
-                const float inv = 1.0f / lt;
-#pragma unroll
-                for (int x = 0; x < 16; ++x) {
-                    const int cc = cv * 32 + acc_row(x, h);
-                    if (cc < dv) *(T*)(ost + ((cc * 8 + qty) * SEGW + (px - x0)) * 2) = (T)(oa[x] * inv);
-                }
-            }
-        }
-        // l, m: by the segment that holds the window's first in-image pixel
-        const int fx = max(w.xs, 0);
-        if (w.ok && vc == 0 && h == 0 && qtx < ws && qty < ws && fx >= x0 && fx < x0 + SEGW) {
-            const int wx = wlo + 2 * p + wl;
-            const int64_t li = qty * ws + qtx + (int64_t)g.T * ((int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b);
-            mo[li] = mt * scale;
-            lo[li] = lt;
-        }
-        lds_barrier();                               // V (over Q|K) read: the next pair may stage
-        if (more) {
-#pragma unroll
-            for (int j = 0; j < NIQ; ++j) { rq[j] = nq[j]; rk[j] = nk[j]; }
-#pragma unroll
-            for (int j = 0; j < NIV; ++j) rv[j] = nv[j];
-        }
-    }
-    __syncthreads();                                 // O staging complete (and the NaN fill, if np = 0)
-    // ---- y: 16-B chunks of the segment's lines (8 pixels of one feature and row) ----
-#pragma unroll
-    for (int i = 0; i < DV * 32 / NTH; ++i) {
-        const int it = tid + NTH * i, c = it & 3, j = (it >> 2) & 7, f = it >> 5;
-        const int y = y0 + j;
-        if (f < dv && j < ws && y >= 0 && y < H_)
-            *(u32x4*)(out + ((int64_t)b * dv + f) * P_ + (int64_t)y * W_ + x0 + 8 * c) =
-                *(const u32x4*)(ost + ((f * 8 + j) * SEGW + 8 * c) * 2);
-    }
 }
 
 // --------------------------------------------------------------------------
@@ -2948,7 +2469,7 @@ static bool rows_f32_ok(const WindowedArgs& a) {
            a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
 }
 
-thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default for small launches), 10 eight-window strip (the default from kStripMin strips on)
+thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default for small launches), 10 eight-window strip (the default from kStripMin strips on); modes 7-9 (the rejected LDS-DMA and segment kernels) were removed in round 4
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
@@ -3029,24 +2550,7 @@ static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStr
             return hipGetLastError();
         }
         const bool two_img_ok = 2 * a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX;
-        const bool seg_ok = a.g.S[0] % 32 == 0 && ((uintptr_t)a.y & 15u) == 0 &&
-                            a.batch * a.g.O[1] * (a.g.S[0] / 32) < INT32_MAX;
-        if (g_win_force_composed == 9 && seg_ok) {   // segment-owning kernel
-            const int64_t nseg = a.batch * a.g.O[1] * (a.g.S[0] / 32);
-            hipLaunchKernelGGL((win_seg<T, D, DV>), dim3((unsigned)nseg), dim3(512), 0, s, (const T*)a.q, (const T*)a.k,
-                               (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e);
-            return hipGetLastError();
-        }
-        if ((g_win_force_composed == 7 || g_win_force_composed == 8) && two_img_ok) {   // LDS-DMA variants
-            if (g_win_force_composed == 7)
-                hipLaunchKernelGGL((win_dma<T, D, DV, 2>), dim3((unsigned)((nw + 1) / 2)), dim3(512), 0, s, (const T*)a.q,
-                                   (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, (int)nw,
-                                   a.scale, a.scale * kLog2e);
-            else
-                hipLaunchKernelGGL((win_dma<T, D, DV, 4>), dim3((unsigned)((nw + 3) / 4)), dim3(1024), 0, s, (const T*)a.q,
-                                   (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d, (int)a.dv, (int)nw,
-                                   a.scale, a.scale * kLog2e);
-        } else if (g_win_force_composed != 3 && two_img_ok) {   // default: register-staged, two windows per workgroup
+        if (g_win_force_composed != 3 && two_img_ok) {   // default: register-staged, two windows per workgroup
             hipLaunchKernelGGL((win_rows1s<T, D, DV, 2>), dim3((unsigned)((nw + 1) / 2)), dim3(512), 0, s,
                                (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
                                (int)a.dv, nw, a.scale, a.scale * kLog2e);

@@ -400,14 +400,15 @@ def test_forward_split_kv(fa, N, Nk, d, dv, B):
     assert_lm_close(_np(l1), _np(l2), "bfloat16", "l split vs unsplit")
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 16, 20])
+@pytest.mark.parametrize("variant", [5, 7, 20, 30])
 @pytest.mark.parametrize("N,Nk,d,dv,B,dtype", [(300, 200, 64, 64, 2, "bfloat16"), (513, 4100, 64, 32, 1, "bfloat16"),
                                                (256, 320, 128, 128, 2, "bfloat16"), (100, 72, 32, 64, 3, "float16"),
                                                (77, 136, 128, 64, 1, "float16"), (1024, 1024, 96, 96, 1, "bfloat16")])
 def test_forced_forward_variants(fa, variant, N, Nk, d, dv, B, dtype):
-    """Every fast-kernel geometry (fa_debug_set_fwd_variant: 32x32x16 MFMA 4..7,
-    16x16x32 MFMA 8, 9, 4 waves/SIMD 16, 20 the defaults with per-element Q / O
-    accesses) against the oracle, ragged Nk and dv != d included."""
+    """Every fast-kernel geometry (fa_debug_set_fwd_variant: 5, 7 the 8-wave 32x32x16
+    kernels, 20 the defaults with per-element Q / O accesses, 30 the one-wave-per-SIMD
+    persistent kernel where its shape rules allow, the defaults elsewhere) against the
+    oracle, ragged Nk and dv != d included."""
     L = fa.lib()
     rng = np.random.default_rng(N * 7 + Nk + d * 3 + dv)
     cast = lambda a: torch.tensor(a).to(DT[dtype]).double().numpy()

@@ -1,8 +1,8 @@
 """GPU parity of every fused windowed-forward kernel, each forced in turn
 (fa_debug_set_win_composed: 1 composed gather→dense→fold, 2 register-gather,
 3 one-window row-shift (ws <= 7) / row-scatter (ws = 8), 4 four-window
-row-staged, 5 one-window row-scatter, 6 two-window row-shift, 7 / 8 two- / four-window LDS-DMA
-with rotated slots and analytic padding columns, 10 the eight-window strip kernel), against the oracle restatement of
+row-staged, 5 one-window row-scatter, 6 two-window row-shift, 10 the eight-window strip kernel
+with rotated slots and analytic padding columns), against the oracle restatement of
 windowed_fa (src/windowed.jl:3-23, NNlib unfold/fold geometry) on geometries
 chosen for the row-staged kernels' edge handling: windows hanging over the
 left / right / bottom image edge, odd and even window x-starts (the row-shift
@@ -45,7 +45,7 @@ def _np(t):
     return t.detach().float().cpu().numpy().astype(np.float64)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10])
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 10])
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
 def test_windowed_forced_path(fa, geom, path):
     W, H, ws, st, pad = geom
@@ -186,7 +186,7 @@ def test_windowed_backward_f32_paths(fa, geom, path):
         L.fa_debug_set_win_composed(old)
 
 
-@pytest.mark.parametrize("path", [0, 3, 6, 7, 8, 10])
+@pytest.mark.parametrize("path", [0, 3, 6, 10])
 def test_windowed_nonfinite_stays_in_its_window(fa, path):
     """An inf in one pixel's k and v reaches only the window holding that pixel, as in
     the reference, where windows are disjoint token sets.  The fused kernels load 8-pixel
@@ -223,52 +223,6 @@ def test_windowed_nonfinite_stays_in_its_window(fa, path):
     assert_lm_close(_np(m)[:, :, keep], mr[:, :, keep], "bfloat16", f"m (path {path})")
 
 
-SEG_GEOMS = [  # width % 32 == 0 (the segment kernel's eligibility)
-    (32, 20, 7, 7, 3),
-    (64, 20, 7, 7, 3),
-    (64, 9, 7, 9, 0),       # stride > ws: uncovered columns and rows are NaN
-    (96, 13, 6, 6, 2),
-    (32, 30, 7, 8, 1),
-    (128, 16, 7, 7, 3),
-    (64, 8, 7, 7, 6),       # pad close to ws
-    (32, 12, 5, 5, 2),
-    (64, 17, 3, 3, 1),
-]
-
-
-@pytest.mark.parametrize("geom", SEG_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
-def test_windowed_segment_kernel(fa, geom):
-    """Mode 9 (win_seg: a workgroup owns a 32-pixel segment of a window row, computes every
-    window meeting it, stores y as 16-B chunks) vs the oracle, and bitwise vs the
-    register-staged two-window kernel (mode 6), which it follows window by window."""
-    W, H, ws, st, pad = geom
-    rng = np.random.default_rng(W * 31 + H * 7 + ws)
-    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
-    L = fa.lib()
-    for (d, dv) in DIMS:
-        B = 3
-        q, k = (bf(rng.standard_normal((W, H, d, B))) for _ in range(2))
-        v = bf(rng.standard_normal((W, H, dv, B)))
-        outs = {}
-        for path in (9, 6):
-            old = L.fa_debug_set_win_composed(path)
-            try:
-                outs[path] = fa.windowed_fa(*(fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v)), ws,
-                                            stride=st, pad=pad)
-                torch.cuda.synchronize()
-            finally:
-                L.fa_debug_set_win_composed(old)
-        y, l, m = outs[9]
-        yr, lr, mr = O.windowed_fa(q, k, v, ws, st, pad)
-        tag = f"d {d} dv {dv}"
-        assert_close(_np(y), yr, "bfloat16", f"y ({tag})", nan_ok=True)
-        assert_lm_close(_np(l), lr, "bfloat16", f"l ({tag})")
-        assert_lm_close(_np(m), mr, "bfloat16", f"m ({tag})")
-        y6, l6, m6 = outs[6]
-        assert torch.equal(y.view(torch.int16), y6.view(torch.int16)), f"y not bitwise equal to mode 6 ({tag})"
-        assert torch.equal(l, l6) and torch.equal(m, m6), f"l, m not bitwise equal to mode 6 ({tag})"
-
-
 STRIP_GEOMS = [  # stride == ws, width % 8 == 0 (the strip kernel's eligibility)
     (32, 20, 7, 7, 3),      # 6 windows: one partial strip
     (128, 16, 7, 7, 3),     # configs[2]'s width: 19 windows = 8 + 8 + 3
@@ -288,8 +242,9 @@ STRIP_GEOMS = [  # stride == ws, width % 8 == 0 (the strip kernel's eligibility)
 @pytest.mark.parametrize("geom", STRIP_GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
 def test_windowed_strip_kernel(fa, geom, dtype):
     """Mode 10 (win_strip: eight adjacent windows per workgroup, channel-streamed LDS-DMA,
-    y stored as 16-B chunks of the strip) vs the oracle, and bitwise vs the two-window
-    LDS-DMA kernel (mode 7), whose rotated-slot arithmetic it repeats window by window."""
+    y stored as 16-B chunks of the strip) vs the oracle, and against the two-window
+    row-shift kernel (mode 6) within one bf16/f16 rounding of y (its fused
+    O·(1/l) rounding differs in the last bit)."""
     W, H, ws, st, pad = geom
     tdt = torch.bfloat16 if dtype == "bfloat16" else torch.float16
     rng = np.random.default_rng(W * 37 + H * 11 + ws)
@@ -300,7 +255,7 @@ def test_windowed_strip_kernel(fa, geom, dtype):
         q, k = (cast(rng.standard_normal((W, H, d, B))) for _ in range(2))
         v = cast(rng.standard_normal((W, H, dv, B)))
         outs = {}
-        for path in (10, 7):
+        for path in (10, 6):
             old = L.fa_debug_set_win_composed(path)
             try:
                 outs[path] = fa.windowed_fa(*(fa.jl_tensor(a, tdt) for a in (q, k, v)), ws, stride=st, pad=pad)
@@ -313,9 +268,10 @@ def test_windowed_strip_kernel(fa, geom, dtype):
         assert_close(_np(y), yr, dtype, f"y ({tag})", nan_ok=True)
         assert_lm_close(_np(l), lr, dtype, f"l ({tag})")
         assert_lm_close(_np(m), mr, dtype, f"m ({tag})")
-        y7, l7, m7 = outs[7]
-        assert torch.equal(y.view(torch.int16), y7.view(torch.int16)), f"y not bitwise equal to mode 7 ({tag})"
-        assert torch.equal(l, l7) and torch.equal(m, m7), f"l, m not bitwise equal to mode 7 ({tag})"
+        y6, l6, m6 = outs[6]
+        assert_close(_np(y), _np(y6), dtype, f"y vs mode 6 ({tag})", nan_ok=True)
+        assert_lm_close(_np(l), _np(l6), dtype, f"l vs mode 6 ({tag})")
+        assert_lm_close(_np(m), _np(m6), dtype, f"m vs mode 6 ({tag})")
 
 
 def test_windowed_strip_full_size(fa):

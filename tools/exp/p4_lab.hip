@@ -6,6 +6,7 @@
 // 7, 8) of its first two blocks; s_memrealtime at kernel start and end for the clock.
 #include <hip/hip_runtime.h>
 __device__ unsigned long long g_p4st[256 * 4 * 64];
+#ifndef P4_NO_STAMP
 #define FA_P4_STAMP(pt, j)                                                                            \
     do {                                                                                              \
         __builtin_amdgcn_sched_barrier(0);                                                            \
@@ -21,6 +22,7 @@ __device__ unsigned long long g_p4st[256 * 4 * 64];
             if ((pt) == 8) ::g_p4st[base_ + 62] = t_;                                                 \
         }                                                                                             \
     } while (0)
+#endif
 #include "../../flashattention.jl_amd/csrc/fa_fwd_p4.hip"
 
 extern "C" int p4_launch(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m, int N,
