@@ -48,6 +48,7 @@ struct BwdParams {
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
     int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
+    const unsigned* sguard = nullptr;          // ... and then only on the slabs b with sguard[b] != 0
 };
 
 template <class T> __device__ __forceinline__ float to_f(T x) { return (float)x; }
@@ -557,10 +558,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_fast(BwdParams p) {
     typedef typename Frag8<T>::half F4;
     constexpr int KB = D * 128, VB = DV * 128, STAGE = KB + VB;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-    // fallback after bwd_fused: recompute dQ only if its hand-off timed out
+    // fallback after bwd_fused: recompute dQ only on the slabs whose hand-off gave up
     if (p.guard && ld_agent((gu32*)(uintptr_t)p.guard) == 0u) return;
     const int lid = xcd_remap(blockIdx.x, p.total_wg);
     const int b = lid / p.nblk, qb = lid - b * p.nblk;
+    if (p.sguard && ld_agent((gu32*)(uintptr_t)(p.sguard + b)) == 0u) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int N = p.N, Nk = p.Nk;
     const auto qrs = bslab<T>(p.Q, (int64_t)b * N * D, (int64_t)N * D);
@@ -849,9 +851,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // vmcnt(0) of a step is the one in the middle of phase A.
 // Every member of a slab must be resident at once: dispatch order within an XCD
 // is monotone, so a slab's members are dealt either to one XCD (K <= 32) or across
-// all of them; each poll is bounded (~20 ms of s_memrealtime), and a timeout sets
-// `err`, which lets the guarded bwd_dq_fast that follows recompute dQ (dK, dV do
-// not depend on the hand-off).
+// all of them.  A poll gives up when its slab is missing members and no more arrive
+// within 50 us (a co-tenant holds the CUs: see wait_count), or after 20 ms; it then
+// sets the slab's trip word and the call's status word `err`; the slab's other polls
+// stop at once, and the guarded bwd_dq_fast that follows recomputes dQ of the slabs
+// that tripped (dK, dV do not depend on the hand-off).
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int sig32(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 
@@ -880,17 +884,42 @@ __device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img,
     }
 }
 
-constexpr uint64_t kSpinTicks = 2000000;   // s_memrealtime (100 MHz): 20 ms
+constexpr uint64_t kSpinTicks = 2000000;   // s_memrealtime (100 MHz): 20 ms, the bound of a poll
+constexpr uint64_t kStallTicks = 5000;     // 50 us: the window of the residency check
 
-// One lane waits until *f >= want; false after a timeout (then *err = 1).
-__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* err) {
+__device__ __forceinline__ void arrive(gu32* p) {
+    __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane waits until *f >= want, or gives up: then the slab's trip word *serr and
+// the call's status word *herr are set, and the slab's other polls stop.  Residency
+// check: every member of the slab adds 1 to *arr when it starts, so while a member is
+// missing the chain may wait on a workgroup that cannot be dispatched until resident
+// ones finish (another process holds CUs).  A poll that has waited one 50-us window
+// trips at once if the slab is still incomplete and no member arrived during that
+// window; a slab whose members are still being dispatched (a second wave behind
+// finishing slabs) keeps arriving, and a complete slab always progresses, so only the
+// 20-ms bound remains for it.
+__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* arr,
+                                           unsigned members) {
     if (ld_agent(f) >= want) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t tw = t0;
+    unsigned seen = ld_agent(arr);
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
-        if (ld_agent(f) >= want || ld_agent(err) != 0u) return;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
-            st_agent(err, 1u);
+        if (ld_agent(f) >= want || ld_agent(serr) != 0u) return;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        bool trip = now - t0 > kSpinTicks;
+        if (now - tw > kStallTicks) {   // one window over: did the slab grow?
+            const unsigned a = ld_agent(arr);
+            trip = trip || (a < members && a == seen);
+            seen = a;
+            tw = now;
+        }
+        if (trip) {
+            st_agent(serr, 1u);
+            st_agent(herr, 1u);
             return;
         }
     }
@@ -1024,6 +1053,9 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     constexpr int NDMA = (D / 8 >= 8 ? D / 64 : 0) + (DV / 8 >= 8 ? DV / 64 : 0);
     gu32* const flg = (gu32*)(p.flags + (int64_t)b * NS);
     gu32* const err = (gu32*)p.err;
+    gu32* const arr = (gu32*)(p.flags + (int64_t)p.batch * NS + b);               // this slab's arrival count
+    gu32* const serr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 1) + b);        // and its trip word
+    if (tid == 0) arrive(arr);
 
     const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
     const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
@@ -1117,7 +1149,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         const bool has_tile = NTQ >= 8 || wave < NTQ;
         if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
-        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, err);
+        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, serr, err, arr, (unsigned)KM);
         __syncthreads();
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
@@ -1171,7 +1203,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // and barriers B2 and B1 order it before every wave's sum loads of that step
         if (wave == 0 && i + 1 < NS && !(abl & 1)) {
             const int tn = slice_of(i + 1), pn = chain_pos(tn);
-            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, err);
+            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, serr, err, arr, (unsigned)KM);
         }
         if (has_tile && !(abl & 10)) {
             pin[0] = load16_sc1_asm<0>(pdesc, pofs);
@@ -1307,6 +1339,7 @@ static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
         p.total_wg = p.nkb * p.batch;
         hipLaunchKernelGGL((bwd_fused<T, D, DV>), dim3((unsigned)p.total_wg), dim3(512), 0, s, p);
         p.guard = p.err;
+        p.sguard = p.flags + (int64_t)p.batch * (p.nqt + 1);
     }
     p.nblk = (p.N + 127) / 128;
     p.total_wg = p.nblk * p.batch;
@@ -1383,7 +1416,7 @@ static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, 
 // K = ceil(Nk/256) members per slab, T = ceil(N/64) slices, step offset 3 (needs
 // 3K <= T); every member of a slab resident at once (K <= CUs; one XCD per slab
 // when K <= CUs/8 and the slab count is a multiple of 8); auto only when the grid
-// fills the chip once.  Workspace: per-slice counters + timeout word, then the
+// fills the chip once.  Workspace: per-slice counters, per-slab arrival counts and trip words, then the
 // running fp32 dQ sums (4·N·d bytes per slab).
 struct FusedPlan {
     bool on = false;
@@ -1407,7 +1440,7 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     f.nkb = (int)K;
     f.nqt = (int)T;
     f.xcd = xcd;
-    f.flag_bytes = al256((size_t)(batch * T) * 4);
+    f.flag_bytes = al256((size_t)(batch * T + 2 * batch) * 4);   // slice counters, slab arrivals + trip words
     f.bytes = f.flag_bytes + al256((size_t)(batch * T * (d / 16)) * 4096) + 256;
     return f;
 }
@@ -1510,20 +1543,23 @@ static hipError_t launch_typed(const BwdParams& p, hipStream_t s, bool fast) {
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
 // Single-pass state in the workspace at w: per-slice counters (zeroed here), then the
-// running dQ sums.  The timeout word is hdr[1], which the pre-pass sets to hdr_err.
+// running dQ sums.  The status word is hdr[1], which the pre-pass sets to hdr_err.
 static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStream_t s) {
     p.flags = (unsigned*)w;
     p.part = (float*)(w + fz.flag_bytes);
     p.nkb = fz.nkb; p.nqt = fz.nqt; p.xcd = fz.xcd;
     p.hdr_plan = 1;
     // mode 3 (tests): the timeout word starts set, so every poll gives up and the
-    // guarded dQ pass must recompute dQ
+    // guarded dQ pass must recompute dQ of every slab
     p.hdr_err = g_bwd_mode == 3 ? 1u : 0u;
 #ifdef FA_BWD_ABL
     p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode == 10 ? 64
              : g_bwd_mode == 11 ? 64 | 3 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;
 #endif
-    return hipMemsetAsync(w, 0, fz.flag_bytes, s);
+    hipError_t e = hipMemsetAsync(w, 0, fz.flag_bytes, s);
+    if (e == hipSuccess && g_bwd_mode == 3)
+        e = hipMemsetD32Async((hipDeviceptr_t)(p.flags + (int64_t)p.batch * (fz.nqt + 1)), 1u, (size_t)p.batch, s);
+    return e;
 }
 
 int dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes, hipStream_t s, int* status,

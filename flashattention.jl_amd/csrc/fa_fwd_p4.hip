@@ -59,6 +59,10 @@ namespace {
 constexpr int kP4Rows = 256;   // query rows per block: 4 waves x 2 x 32
 constexpr int kP4KS = 3;       // K ring slots (K(t+3) issued in phase B(t))
 constexpr int kP4VS = 2;       // V ring slots (V(t+1) issued in phase B(t))
+#ifndef FA_P4_PF
+#define FA_P4_PF 4
+#endif
+constexpr int kP4Prefetch = FA_P4_PF;   // MFMA slots an LDS operand read runs ahead (LDS latency ~100+ cycles)
 
 __device__ __forceinline__ uint32_t p4_lds(const void* ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)ptr;
@@ -323,7 +327,8 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         int ko[2] = {koff[0], koff[1]};
         int vo[2][2] = {{voff[0][0], voff[0][1]}, {voff[1][0], voff[1][1]}};
         asm volatile("" : "+v"(ko[0]), "+v"(ko[1]), "+v"(vo[0][0]), "+v"(vo[0][1]), "+v"(vo[1][0]), "+v"(vo[1][1]));
-        F8 fr[3];
+        constexpr int PF = kP4Prefetch;   // LDS operand reads run PF MFMA slots ahead
+        F8 fr[PF + 1];
         auto rd = [&](int i) __attribute__((always_inline)) {
             if ((FA_P4_ABL & 4) && i >= 2 && (PV || QK) && NM > 8) return;
             if (i < NKQ) {
@@ -331,14 +336,13 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
                 const char* a = kslot + ko[kb] + 16 * s * 128;
                 const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
                 const F4 hi = __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
-                fr[i % 3] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                fr[i % (PF + 1)] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
             } else {
                 const int j = i - NKQ, cb = j >> 2, kb = (j >> 1) & 1, s = j & 1;
-                fr[i % 3] = *(const F8*)(vslot + cb * 32 * 128 + vo[kb][s]);
+                fr[i % (PF + 1)] = *(const F8*)(vslot + cb * 32 * 128 + vo[kb][s]);
             }
         };
-        rd(0);
-        if (NM > 1) rd(1);
+        p4_static_for<(PF < NM ? PF : NM)>([&](auto It) __attribute__((always_inline)) { rd(decltype(It)::value); });
         p4_fence();
         p4_static_for<NM>([&](auto It) __attribute__((always_inline)) {
             constexpr int i = decltype(It)::value;
@@ -346,13 +350,13 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
                 mid();
                 p4_fence();
             }
-            if constexpr (i + 2 < NM) rd(i + 2);
+            if constexpr (i + PF < NM) rd(i + PF);
             if constexpr (i < NKQ) {
                 constexpr int kb = i / C::NKS, s = i % C::NKS;
-                p4_mfma_s(S[u][kb], fr[i % 3], qf[u][s], s == 0);
+                p4_mfma_s(S[u][kb], fr[i % (PF + 1)], qf[u][s], s == 0);
             } else {
                 constexpr int j = i - NKQ, cb = j >> 2, kb = (j >> 1) & 1, s = j & 1;
-                oacc[u][cb] = mfma32x32x16(fr[i % 3], __builtin_bit_cast(F8, P[u][kb][s]), oacc[u][cb]);
+                oacc[u][cb] = mfma32x32x16(fr[i % (PF + 1)], __builtin_bit_cast(F8, P[u][kb][s]), oacc[u][cb]);
             }
             valu(i);
             p4_fence();

@@ -1745,17 +1745,28 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
         }
     };
 
-    // Strips are dealt dynamically: workgroup b takes strips b and b + G (G = the grid,
-    // one workgroup per CU), then 2G + c for each c it draws from the counter `ctr`
-    // (zeroed by the launcher).  Workgroups start up to ~20 us apart and run at
-    // different speeds; a static deal of 8 strips each left ~11 % of the CUs idle and
+    // Strips are dealt dynamically within XCD groups.  Workgroup b belongs to group
+    // x = b mod 8 (the XCD the dispatcher deals it to), and group x owns the contiguous
+    // strip range [lo, hi), sized in proportion to its M workgroups (>= M strips, as
+    // nstrip >= G): its workgroup l takes strips lo + l and lo + l + M, then lo + 2M + c
+    // for each c it draws from the group's counter (zeroed by the launcher, 64 B apart).
+    // So neighbouring strips of a window row, which share the 128-B lines at their ends,
+    // run at about the same time on one XCD and meet in its L2 (dealt chip-wide, each
+    // shared line was fetched once per XCD that touched it: 2.0x the algorithmic bytes
+    // in FETCH_SIZE, r03_win_strip_pmc.txt).  Workgroups start up to ~20 us apart and run
+    // at different speeds; a static deal of 8 strips each left ~11 % of the CUs idle and
     // a ~20 us tail.  The draw for the strip after next is issued by lane 0 of wave 0
     // right after a strip's first wait and counted as a vector-memory op; its answer is
     // certain to have landed at the next strip's first wait (every DMA of that strip was
     // issued after it), where it is broadcast through LDS.
     const int G = (int)gridDim.x;
-    int sid = blockIdx.x;
-    int nsid = sid + G;                              // the strip after cur
+    const int NG = G < 8 ? G : 8, grp = (int)blockIdx.x % NG;
+    const int M = G / NG + (grp < G % NG ? 1 : 0);   // workgroups of the group
+    auto cum = [&](int x) { return x * (G / NG) + min(x, G % NG); };   // workgroups of groups < x
+    const int lo = (int)((int64_t)nstrip * cum(grp) / G), hi = (int)((int64_t)nstrip * cum(grp + 1) / G);
+    unsigned* const gctr = ctr + 16 * grp;
+    int sid = lo + (int)blockIdx.x / NG;
+    int nsid = sid + M;                              // the strip after cur
     unsigned drawn = 0u;                             // lane 0 of wave 0: the counter's last answer
     StripPos cur = pos_of(sid);
 #pragma unroll
@@ -1777,7 +1788,7 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
     };
     const F8 id0 = ident(0), id1 = ident(1);
 
-    for (int it = 0; sid < nstrip; ++it) {
+    for (int it = 0; sid < hi; ++it) {
         [[maybe_unused]] const int fa_sid = sid;
         FA_BSTAMP(0);
         tid = threadIdx.x;
@@ -1795,7 +1806,7 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
             wait_vm(vm_issued - mark_of(slot_of(j)));
             if (j == 0 && it > 0 && wave == 0) {
                 asm volatile("" : "+v"(drawn));          // landed with this wait (see the deal above)
-                if (lane == 0) lds_w32u(nsid_lds, 2u * (unsigned)G + drawn);
+                if (lane == 0) lds_w32u(nsid_lds, (unsigned)(lo + 2 * M) + drawn);
             }
             lds_barrier();
             if (j == 0) {
@@ -1805,10 +1816,10 @@ __global__ __launch_bounds__(512, 1) void win_bwd_strip(const T* __restrict__ q,
                     asm volatile("" : "+v"(nsid));
                     nsid = __builtin_amdgcn_readfirstlane(nsid);
                 }
-                has_next = nsid < nstrip;
+                has_next = nsid < hi;
                 nxt = has_next ? pos_of(nsid) : cur;
                 if (wave == 0) {                         // draw the strip after nsid
-                    if (lane == 0) drawn = atomic_add_ret(ctr, 1u);
+                    if (lane == 0) drawn = atomic_add_ret(gctr, 1u);
                     vm_issued += 1;
                 }
             }
@@ -2889,18 +2900,18 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
     if (bwd_strip_ok(a)) {
         const int k0 = strip_first(a.g);
         const int64_t nsx = strip_count(a.g, k0), nstrip = nsx * a.g.O[1] * a.batch;
-        // persistent: one workgroup per CU, strips dealt by a counter in the workspace
+        // persistent: one workgroup per CU, strips dealt by 8 XCD-group counters in the workspace
         const int64_t cus = device_cus(s) > 0 ? device_cus(s) : 256;
         const int64_t grid = nstrip < cus ? nstrip : cus;
-        // the counter is an atomic word: round its address up to 256 B as the dense
+        // the counters are atomic words: round their address up to 256 B as the dense
         // backward does (the header allows any workspace alignment; windowed_workspace
-        // reserves the 256-B slack)
+        // reserves the 256-B slack, and its buffers are far larger than the 512 B used)
         unsigned* const ctr = (unsigned*)(((uintptr_t)a.workspace + 255) & ~(uintptr_t)255);
-        if (!a.workspace || a.workspace_bytes < (size_t)((char*)ctr - (char*)a.workspace) + 4) {
-            *why = "workspace missing (the strip backward keeps its strip counter there)";
+        if (!a.workspace || a.workspace_bytes < (size_t)((char*)ctr - (char*)a.workspace) + 512) {
+            *why = "workspace missing (the strip backward keeps its strip counters there)";
             return FA_ERR_WORKSPACE;
         }
-        if ((e = hipMemsetAsync(ctr, 0, 4, s)) != hipSuccess) {
+        if ((e = hipMemsetAsync(ctr, 0, 512, s)) != hipSuccess) {   // 8 group counters, 64 B apart
             *why = hipGetErrorString(e);
             return FA_ERR_HIP;
         }

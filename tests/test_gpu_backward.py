@@ -295,8 +295,12 @@ def test_backward_handoff_status_errors(fa):
 def test_backward_two_streams_concurrent(fa):
     """Two configs[3]-sized backward calls (N 8192, d 128, 64 slabs) on two streams at
     once: each single pass needs all 32 members of a slab resident, and the other
-    stream holds CUs.  Both results match the float64 oracle on one slab each; the
-    hand-off status of each call is reported (a timeout is correct but slow)."""
+    stream holds CUs, so slabs of the two calls can wait on each other's CUs.  The
+    residency check (fa_bwd.hip wait_count) must trip such a slab within tens of us and
+    recompute only its dQ: the pair's wall time stays within 1.6x the same two calls
+    run back to back on one stream (a 20-ms poll bound would cost ~7x), and both
+    results match the float64 oracle on one slab each."""
+    import time
     N, d, BH = 8192, 128, 64
     g = torch.Generator(device="cuda").manual_seed(23)
     mk = lambda: fa.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
@@ -307,16 +311,31 @@ def test_backward_two_streams_concurrent(fa):
         ins.append((Q, K, V, Oo, dO, l, m))
     torch.cuda.synchronize()
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    outs, status = [None, None], [None, None]
-    for i in range(2):
-        with torch.cuda.stream(streams[i]):
-            outs[i] = fa.dense_fa_backward(*ins[i])
-    for i in range(2):
-        with torch.cuda.stream(streams[i]):
-            status[i] = fa.backward_handoff_status()
-    torch.cuda.synchronize()
-    print(f"two-stream backward hand-off status: {status}")
-    assert all(s in (-1, 0, 1) for s in status)
+
+    def pair(concurrent):
+        outs = [None, None]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(2):
+            with torch.cuda.stream(streams[i if concurrent else 0]):
+                outs[i] = fa.dense_fa_backward(*ins[i])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        status = []
+        for i in range(2 if concurrent else 1):
+            with torch.cuda.stream(streams[i]):
+                status.append(fa.backward_handoff_status())
+        return outs, status, dt
+
+    pair(False); pair(True)   # warm up (allocations, code objects, clocks)
+    serial = min(pair(False)[2] for _ in range(3))
+    runs = [pair(True) for _ in range(3)]
+    outs, status, _ = runs[-1]
+    conc = min(r[2] for r in runs)
+    print(f"two-stream backward: serial pair {serial * 1e3:.2f} ms, concurrent pair "
+          f"{[round(r[2] * 1e3, 2) for r in runs]} ms, hand-off status {[r[1] for r in runs]}")
+    assert all(s in (-1, 0, 1) for r in runs for s in r[1])
+    assert conc <= 1.6 * serial, f"concurrent pair {conc * 1e3:.2f} ms vs serial {serial * 1e3:.2f} ms"
     for i, b in ((0, 5), (1, 40)):
         Q, K, V, Oo, dO, l, m = ins[i]
         sl = lambda t: _np(t[:, :, b:b + 1])

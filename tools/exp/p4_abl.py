@@ -1,8 +1,9 @@
-"""Time the p4 forward's timing-only ablations (tools/exp/p4_abl.sh builds
-libp4_lab_a<N>.so; FA_P4_ABL bits: 1 no K/V/Q DMA in the tile loop, 2 no exponentials,
-4 no LDS operand reads, 8 no softmax/max VALU) against the default kernel (variant 0)
-in one process, interleaved rounds after a clock settle.  WRONG results by design.
-Usage: python tools/exp/p4_abl.py N,d,BH abl...   (e.g. 4096,64,64 0 1 2 4 8 15)"""
+"""Time diagnostic builds of the p4 forward (tools/exp/p4_abl.sh builds
+libp4_lab_<tag>.so: FA_P4_ABL timing-only ablations — 1 no K/V/Q DMA in the tile loop,
+2 no exponentials, 4 no LDS operand reads, 8 no softmax/max VALU; WRONG results by
+design — or other -D settings) against the default kernel (variant 0) in one process,
+interleaved rounds after a clock settle.
+Usage: python tools/exp/p4_abl.py N,d,BH tag...   (e.g. 4096,64,64 a0 a1 pf2)"""
 import ctypes, os, sys, time
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
@@ -11,9 +12,9 @@ import numpy as np, torch
 import fa_hip
 
 N, d, BH = (int(x) for x in sys.argv[1].split(","))
-abls = [int(a) for a in sys.argv[2:]] or [0]
+abls = sys.argv[2:] or ["a0"]
 L = fa_hip.lib()
-libs = {a: ctypes.CDLL(os.path.join(HERE, f"libp4_lab_a{a}.so")) for a in abls}
+libs = {a: ctypes.CDLL(os.path.join(HERE, f"libp4_lab_{a}.so")) for a in abls}
 P = lambda t: ctypes.c_void_p(t.data_ptr())
 g = torch.Generator(device="cuda").manual_seed(0)
 Q, K, V = (fa_hip.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16) for _ in range(3))
@@ -23,7 +24,7 @@ st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 flops = 4.0 * BH * N * N * d
 fns = {"v0": lambda: fa_hip.dense_fa_(O, l, m, Q, K, V)}
 for a, lib in libs.items():
-    fns[f"abl{a}"] = (lambda lib: lambda: lib.p4_launch(1, P(Q), P(K), P(V), P(O), P(l), P(m), N, d, BH, st))(lib)
+    fns[a] = (lambda lib: lambda: lib.p4_launch(1, P(Q), P(K), P(V), P(O), P(l), P(m), N, d, BH, st))(lib)
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < 1.0:
     for f in fns.values():

@@ -1,9 +1,11 @@
 #!/bin/bash
-# Build the timing-only ablation variants of the p4 forward (tools/exp/p4_lab.hip with
-# FA_P4_ABL) as libp4_lab_a<N>.so.  Usage: bash tools/exp/p4_abl.sh 0 1 2 4 8
+# Build diagnostic variants of the p4 forward (tools/exp/p4_lab.hip) as libp4_lab_<tag>.so.
+# Each argument is TAG=FLAGS, e.g.  a0="-DFA_P4_ABL=0"  pf2="-DFA_P4_PF=2"
+# (FA_P4_ABL timing-only ablation bits: see fa_fwd_p4.hip).
 cd "$(dirname "$0")"
-for a in "$@"; do
+for arg in "$@"; do
+  tag="${arg%%=*}"; flags="${arg#*=}"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared -fno-gpu-rdc -fno-slp-vectorize \
-    -DFA_P4_ABL=$a -DP4_NO_STAMP -o libp4_lab_a$a.so p4_lab.hip &
+    -DP4_NO_STAMP $flags -o libp4_lab_$tag.so p4_lab.hip &
 done
 wait
