@@ -480,7 +480,7 @@ def cpu_baseline(node: bool = False):
                       f"threads, median of 3: {bl['configs1_s']:.3f} s; 'legs' adds configs[0] and the "
                       f"reference's Float64 case" + ("" if node else
                       f"; the node-wide legs (all {ncpu} CPUs) run with bench.py --cpu-node "
-                      f"(profiles/r03_cpu_baseline_node.log)"),
+                      f"(profiles/r04_cpu_baseline_node.log)"),
             "legs": legs,
             "reference_published": "dense_fa Julia N=512 d=64 bs=1 Float64: 2.392 ms, unstated CPU "
                                    "(/root/reference/logs/compare1.txt:4)"}

@@ -150,6 +150,16 @@ int fa_debug_set_bwd_mode(int v) {
     return old;
 }
 
+// Not part of the public header: 1 = the single-pass backward hands its running dQ sums
+// over in the XCD's L2 when all of a slab's members run on one XCD (plain stores instead
+// of sc1 write-through); returns the previous value.
+int fa_debug_set_bwd_l2local(int v) {
+    const int old = fa::g_bwd_l2local;
+    if (v < 0 || v > 1) return -1;
+    fa::g_bwd_l2local = v;
+    return old;
+}
+
 // Not part of the public header: circulant kernel override (1 one-wave-per-query,
 // 2 LDS-tiled SIMT; 0 auto).
 int fa_debug_set_circ_generic(int v) {

@@ -46,6 +46,7 @@ struct BwdParams {
     unsigned hdr_plan = 0, hdr_err = 0;
     float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
+    int l2local = 0;  // 1: hand the running sums over in the XCD's L2 when a slab's members share one
     int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
     const unsigned* sguard = nullptr;          // ... and then only on the slabs b with sguard[b] != 0
@@ -1055,7 +1056,15 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     gu32* const err = (gu32*)p.err;
     gu32* const arr = (gu32*)(p.flags + (int64_t)p.batch * NS + b);               // this slab's arrival count
     gu32* const serr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 1) + b);        // and its trip word
-    if (tid == 0) arrive(arr);
+    gu32* const xmask = (gu32*)(p.flags + (int64_t)p.batch * (NS + 2) + b);       // the XCDs of its members
+    if (tid == 0) {
+        if (p.l2local) {   // this member's XCD into the slab's mask, acknowledged before it counts as arrived
+            const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID[3:0]
+            __hip_atomic_fetch_or(xmask, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        arrive(arr);
+    }
 
     const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
     const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
@@ -1128,6 +1137,23 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const int ktb = wave & 1;
     const int dsrow = 32 * wave + sig32(r);                  // this lane's dSᵀ row
     const int cbq = wave % (D / 32), uq = wave / (D / 32);   // this wave's dQᵀ tile (wave < NTQ)
+
+    // L2-local hand-off: when every member of the slab runs on one XCD (the xcd mapping
+    // deals them so; the mask checks it), the running sums are stored plainly and stay in
+    // that XCD's L2, where the next member's sc1 loads (L1 bypass, L2-served) find them;
+    // otherwise sc1 stores (L2 write-through, dropped) as everywhere else.  Decided once
+    // every member has arrived (a stalled arrival trips the slab as in wait_count).
+    __shared__ unsigned s_local;
+    bool local = false;
+    if (p.l2local) {
+        if (tid == 0) {
+            wait_count(arr, (unsigned)KM, serr, err, arr, (unsigned)KM);
+            const unsigned m = ld_agent(xmask);
+            s_local = (ld_agent(arr) >= (unsigned)KM && (m & (m - 1u)) == 0u) ? 1u : 0u;
+        }
+        __syncthreads();
+        local = s_local != 0u;
+    }
 
     int t_prev = 0, pos_prev = 0;
     bool pub_prev = false;
@@ -1297,7 +1323,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 for (int c4 = 0; c4 < 4; ++c4) {
                     const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
                                       __float_as_uint(acc[4 * c4 + 2]), __float_as_uint(acc[4 * c4 + 3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);   // sc1
+                    if (local) __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 0);
+                    else __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);   // sc1
                 }
             }
         }
@@ -1331,6 +1358,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
 thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
+thread_local int g_bwd_l2local = 0;         // bwd_fused: L2-local hand-off when a slab sits on one XCD
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
@@ -1416,7 +1444,7 @@ static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, 
 // K = ceil(Nk/256) members per slab, T = ceil(N/64) slices, step offset 3 (needs
 // 3K <= T); every member of a slab resident at once (K <= CUs; one XCD per slab
 // when K <= CUs/8 and the slab count is a multiple of 8); auto only when the grid
-// fills the chip once.  Workspace: per-slice counters, per-slab arrival counts and trip words, then the
+// fills the chip once.  Workspace: per-slice counters, per-slab arrival counts, trip words and XCD masks, then the
 // running fp32 dQ sums (4·N·d bytes per slab).
 struct FusedPlan {
     bool on = false;
@@ -1440,7 +1468,7 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     f.nkb = (int)K;
     f.nqt = (int)T;
     f.xcd = xcd;
-    f.flag_bytes = al256((size_t)(batch * T + 2 * batch) * 4);   // slice counters, slab arrivals + trip words
+    f.flag_bytes = al256((size_t)(batch * T + 3 * batch) * 4);   // slice counters; slab arrivals, trip words, XCD masks
     f.bytes = f.flag_bytes + al256((size_t)(batch * T * (d / 16)) * 4096) + 256;
     return f;
 }
@@ -1552,6 +1580,7 @@ static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStr
     // mode 3 (tests): the timeout word starts set, so every poll gives up and the
     // guarded dQ pass must recompute dQ of every slab
     p.hdr_err = g_bwd_mode == 3 ? 1u : 0u;
+    p.l2local = g_bwd_l2local;
 #ifdef FA_BWD_ABL
     p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode == 10 ? 64
              : g_bwd_mode == 11 ? 64 | 3 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;

@@ -1056,7 +1056,9 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
         (int64_t)p.ldk * a.dv * esz >= (int64_t)INT32_MAX)
         p.fast = 0;
     // split-KV for small grids (fast kernels, default geometry, workspace given)
-    if (p.fast && (g_fwd_variant == 0 || g_fwd_variant == 30) && a.workspace) {
+    // (variant 30: not when fa_fwd_p4's own 256-row blocks already fill the chip)
+    const bool p4_fills = g_fwd_variant == 30 && (a.N + 255) / 256 * a.batch >= device_cus(s);
+    if (p.fast && (g_fwd_variant == 0 || g_fwd_variant == 30) && !p4_fills && a.workspace) {
         const SplitPlan sp = split_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
         if (sp.nsplit > 1 && a.workspace_bytes >= pad_bytes + sp.bytes) {
             auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };

@@ -47,7 +47,8 @@
 #endif
 // FA_P4_ABL: timing-only ablations of the diagnostic build (WRONG results): 1 no K/V/Q
 // DMA in the tile loop, 2 no exponentials, 4 no LDS operand reads in the tile loop,
-// 8 no softmax / max VALU work at all.
+// 8 no softmax / max VALU work at all, 16 one transposed read per K fragment (of two),
+// 32 no V fragment reads.
 #ifndef FA_P4_ABL
 #define FA_P4_ABL 0
 #endif
@@ -363,6 +364,69 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         });
         if constexpr (NPRE >= NM) mid();
     };
+    // Both phases of a tile in one stream: X = query block 0's MFMAs with valx / midx,
+    // then Y = block 1's with valy / midy (same kinds of MFMA, so the same K / V fragments
+    // in the same order: block 1 reads what block 0 read).  The operand prefetch runs on
+    // across the seam, so Y's first reads are in flight under X's last MFMAs instead of
+    // waited for at Y's start; seam() runs between the two.
+    auto phase2 = [&](auto QKt, auto PVt, auto NPXt, auto NPYt, const char* kslot, const char* vslot, auto&& valx,
+                      auto&& midx, auto&& seam, auto&& valy, auto&& midy) __attribute__((always_inline)) {
+        constexpr bool QK = decltype(QKt)::value, PV = decltype(PVt)::value;
+        constexpr int NPX = decltype(NPXt)::value, NPY = decltype(NPYt)::value;
+        constexpr int NKQ = QK ? C::NKQ : 0;
+        constexpr int NM = NKQ + (PV ? C::NVQ : 0);
+        int ko[2] = {koff[0], koff[1]};
+        int vo[2][2] = {{voff[0][0], voff[0][1]}, {voff[1][0], voff[1][1]}};
+        asm volatile("" : "+v"(ko[0]), "+v"(ko[1]), "+v"(vo[0][0]), "+v"(vo[0][1]), "+v"(vo[1][0]), "+v"(vo[1][1]));
+        constexpr int PF = kP4Prefetch;
+        F8 fr[PF + 1];
+        auto rd = [&](int i) __attribute__((always_inline)) {
+            const int f = i % NM;
+            if ((FA_P4_ABL & 4) && f >= 2 && NM > 8) return;
+            if ((FA_P4_ABL & 32) && f >= NKQ && f >= 2) return;
+            if (f < NKQ) {
+                const int kb = f / C::NKS, s = f % C::NKS;
+                const char* a = kslot + ko[kb] + 16 * s * 128;
+                const F4 lo = __builtin_bit_cast(F4, ds_read_tr16(a));
+                const F4 hi = (FA_P4_ABL & 16) ? lo : __builtin_bit_cast(F4, ds_read_tr16(a + 4 * 128));
+                fr[i % (PF + 1)] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            } else {
+                const int j = f - NKQ, cb = j >> 2, kb = (j >> 1) & 1, s = j & 1;
+                fr[i % (PF + 1)] = *(const F8*)(vslot + cb * 32 * 128 + vo[kb][s]);
+            }
+        };
+        p4_static_for<(PF < NM ? PF : NM)>([&](auto It) __attribute__((always_inline)) { rd(decltype(It)::value); });
+        p4_fence();
+        p4_static_for<2 * NM>([&](auto It) __attribute__((always_inline)) {
+            constexpr int i = decltype(It)::value;
+            constexpr int u = i / NM, k = i % NM;
+            if constexpr (u == 0 && k == NPX) {
+                midx();
+                p4_fence();
+            }
+            if constexpr (u == 1 && k == NPY) {
+                midy();
+                p4_fence();
+            }
+            if constexpr (i + PF < 2 * NM) rd(i + PF);
+            if constexpr (k < NKQ) {
+                constexpr int kb = k / C::NKS, s = k % C::NKS;
+                p4_mfma_s(S[u][kb], fr[i % (PF + 1)], qf[u][s], s == 0);
+            } else {
+                constexpr int j = k - NKQ, cb = j >> 2, kb = (j >> 1) & 1, s = j & 1;
+                oacc[u][cb] = mfma32x32x16(fr[i % (PF + 1)], __builtin_bit_cast(F8, P[u][kb][s]), oacc[u][cb]);
+            }
+            if constexpr (u == 0) valx(k);
+            else valy(k);
+            p4_fence();
+            if constexpr (i == NM - 1) {
+                if constexpr (NPX >= NM) midx();
+                seam();
+                p4_fence();
+            }
+        });
+        if constexpr (NPY >= NM) midy();
+    };
     auto none = [](int) __attribute__((always_inline)) {};
     auto nomid = []() __attribute__((always_inline)) {};
 
@@ -434,53 +498,52 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         const u32x4 vds = p4_desc(vn ? vp1 : vp0, vn ? vn1 : vbytes), kds = p4_desc(kn ? kp1 : kp0, kn ? kn1 : kbytes);
         const int jv2 = vn ? jv - NT : jv, jk2 = kn ? jk - NT : jk;
         FA_P4_STAMP(2, j);
-        {   // ---- X: block 0 MFMAs ∥ block 1 softmax (tile j) ----
-            MaxQB mx;
-            SoftmaxQB<T> sm;
-            sm.c = c;
-            auto side = softmax_side(std::conditional_t<LAST, NMvt, NMt>{}, std::conditional_t<LAST, NPvt, NPt>{}, 1, mx, sm);
-            auto valu = [&](int i) __attribute__((always_inline)) {
-                side(i);
-                // V(j+1) pieces and the Q piece early in the phase
-                constexpr int NMx = LAST ? C::NVQ : NMF;
-                constexpr int NPx = LAST ? (C::NVQ >= 16 ? 4 : 2) : NPRE;
-                if (FA_P4_ABL & 1) return;
-                if (i >= NPx && i < NPx + C::VP) dma_v1(vds, vs0 ^ 1, jv2, i - NPx);
-                if (i == NPx + C::VP) {
-                    const bool qv = j < C::QP;
-                    dma_q1(p4_desc(qpn, qv ? qnn : 0u), qbn, qv ? j : 0, qv ? qdst(j) : lds0 + C::OOFF + (uint32_t)wave * C::OST);
-                }
-                (void)NMx;
-            };
-            auto mid = [&]() __attribute__((always_inline)) {
-                decide(1, mx.mt);
-                sm.nmc = -m_used[1] * c;
-            };
-            phase(std::integral_constant<bool, !LAST>{}, Yes{}, std::conditional_t<LAST, NPvt, NPt>{}, 0, kslot, vslot, valu, mid);
-            l_run[1] += sm.sum();
-        }
-        FA_P4_STAMP(3, j);
-        if constexpr (!LAST) {   // ---- Y: block 1 MFMAs ∥ block 0 softmax (tile j+1) ----
-            MaxQB mx;
-            SoftmaxQB<T> sm;
-            sm.c = c;
-            auto side = softmax_side(NMt{}, NPt{}, 0, mx, sm);
-            auto valu = [&](int i) __attribute__((always_inline)) {
-                side(i);
+        // ---- X: block 0 MFMAs ∥ block 1 softmax (tile j); Y: block 1 MFMAs ∥ block 0
+        //      softmax (tile j+1), or on the last tile block 1's PV only ----
+        constexpr int NMx = LAST ? C::NVQ : NMF;
+        constexpr int NPx = LAST ? (C::NVQ >= 16 ? 4 : 2) : NPRE;
+        MaxQB mx1, mx0;
+        SoftmaxQB<T> sm1, sm0;
+        sm1.c = c;
+        sm0.c = c;
+        auto side1 = softmax_side(std::conditional_t<LAST, NMvt, NMt>{}, std::conditional_t<LAST, NPvt, NPt>{}, 1, mx1, sm1);
+        auto side0 = softmax_side(NMt{}, NPt{}, 0, mx0, sm0);
+        auto valx = [&](int i) __attribute__((always_inline)) {
+            side1(i);
+            // V(j+1) pieces and the Q piece early in the phase
+            if (FA_P4_ABL & 1) return;
+            if (i >= NPx && i < NPx + C::VP) dma_v1(vds, vs0 ^ 1, jv2, i - NPx);
+            if (i == NPx + C::VP) {
+                const bool qv = j < C::QP;
+                dma_q1(p4_desc(qpn, qv ? qnn : 0u), qbn, qv ? j : 0, qv ? qdst(j) : lds0 + C::OOFF + (uint32_t)wave * C::OST);
+            }
+        };
+        auto midx = [&]() __attribute__((always_inline)) {
+            decide(1, mx1.mt);
+            sm1.nmc = -m_used[1] * c;
+        };
+        auto seam = [&]() __attribute__((always_inline)) {
+            l_run[1] += sm1.sum();
+            FA_P4_STAMP(3, j);
+        };
+        auto valy = [&](int i) __attribute__((always_inline)) {
+            if constexpr (!LAST) {
+                side0(i);
                 if (!(FA_P4_ABL & 1) && i >= NPRE && i < NPRE + C::KP) dma_k1(kds, ks0, jk2, i - NPRE);
-            };
-            auto mid = [&]() __attribute__((always_inline)) {
-                decide(0, mx.mt);
-                sm.nmc = -m_used[0] * c;
-            };
-            phase(Yes{}, Yes{}, NPt{}, 1, kslot, vslot, valu, mid);
-            l_run[0] += sm.sum();
-        } else {                 // ---- last tile: block 1's PV only; K(j+3) still goes out ----
-            auto valu = [&](int i) __attribute__((always_inline)) {
+            } else {
                 if (!(FA_P4_ABL & 1) && i < C::KP) dma_k1(kds, ks0, jk2, i);
-            };
-            phase(No{}, Yes{}, std::integral_constant<int, 1000>{}, 1, kslot, vslot, valu, nomid);
-        }
+            }
+        };
+        auto midy = [&]() __attribute__((always_inline)) {
+            if constexpr (!LAST) {
+                decide(0, mx0.mt);
+                sm0.nmc = -m_used[0] * c;
+            }
+        };
+        phase2(std::integral_constant<bool, !LAST>{}, Yes{}, std::integral_constant<int, NPx>{},
+               std::integral_constant<int, LAST ? 1000 : NPRE>{}, kslot, vslot, valx, midx, seam, valy, midy);
+        if constexpr (!LAST) l_run[0] += sm0.sum();
+        (void)NMx;
         FA_P4_STAMP(5, j);
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::KP) : "memory");
         FA_P4_STAMP(6, j);

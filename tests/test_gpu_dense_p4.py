@@ -21,6 +21,15 @@ from oracle import fa_oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module")
+def fa():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    import fa_hip
+    fa_hip.lib()
+    return fa_hip
+
+
 def _np(t):
     return t.float().cpu().double().numpy()
 
