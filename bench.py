@@ -59,6 +59,7 @@ reduction; the JSON then says "cpu_step_hook": true.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -269,8 +270,17 @@ def cfg4_block(fa, world, rank, dist, steps, warmup, cpu_hook=False):
         r = sharded_strong(make_step, CFG4_SLABS, world, rank, dist, steps, warmup, 4.0 * N * N * d)
         torch.cuda.empty_cache()
     r["workload"] = "configs[4]: dense_fa bf16 forward, (B,H,N,d)=(64,16,16384,128), 1024 slabs split over ranks"
-    r["kernel"] = "fa::dense_fwd_w8b64_wide<bf16,128,128>"
+    r["kernel"] = "(cpu hook)" if cpu_hook else _fwd_kernel_128(fa)
     return r
+
+
+def _fwd_kernel_128(fa):
+    """The d = 128 forward kernel the last dense_fa_ call ran (fa_debug_fwd_last_path:
+    30 = the one-wave-per-SIMD persistent kernel fa_fwd_p4.hip, else the 8-wave one)."""
+    L = fa.lib()
+    L.fa_debug_fwd_last_path.restype = ctypes.c_int
+    return ("fa::dense_fwd_p4<bf16,128,128>" if L.fa_debug_fwd_last_path() == 30
+            else "fa::dense_fwd_w8b64_wide<bf16,128,128>")
 
 
 def _mfma_roofline(flops, seconds, kernel, note=None):
@@ -298,6 +308,7 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
     f = 4.0 * BH * N * N * d
     _, e_f = time_region(lambda: fa.dense_fa_(O, l, m, Q, K, V), steps_fwd, 2, dist)
     t_f = e_f / steps_fwd
+    k_f = _fwd_kernel_128(fa)
     _, e_b = time_region(lambda: fa.dense_fa_backward(Q, K, V, O, dO, l, m), steps_bwd, 1, dist)
     t_b = e_b / steps_bwd
     hs = fa.backward_handoff_status(Q.device)   # the last timed call
@@ -312,7 +323,7 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
         "fwd_tflops": f / t_f / 1e12, "bwd_tflops": 2.5 * f / t_b / 1e12,
         "fwd_bwd_tflops": 3.5 * f / (t_f + t_b) / 1e12,
         "fwd_ms": t_f * 1e3, "bwd_ms": t_b * 1e3, "steps_fwd": steps_fwd, "steps_bwd": steps_bwd,
-        "roofline_fwd": _mfma_roofline(f, t_f, "fa::dense_fwd_w8b64_wide<bf16,128,128>"),
+        "roofline_fwd": _mfma_roofline(f, t_f, k_f),
         "roofline_bwd": _mfma_roofline(
             2.5 * f, t_b, "fa::bwd_fused<bf16,128,128>",
             "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + bwd_fused + the guarded dQ pass), "

@@ -876,7 +876,10 @@ bool launch_dense_fwd_p4(const FwdParams& p, int Dc, int DVc, int dtype, hipStre
 template <class T, int D>
 static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
     g_fwd_last_path = 0;
-    if (p.fast && g_fwd_variant == 30) {   // one wave per SIMD, persistent (fa_fwd_p4.hip)
+    // one wave per SIMD, persistent (fa_fwd_p4.hip): the default at d = dv = 128 (5-8 %
+    // over the 8-wave kernel, bitwise equal: profiles/r04_fwd_p4_default_d128_ab.log);
+    // at 64 the 8-wave kernel stays (p4 is 15 % slower there); variant 30 forces it
+    if (p.fast && (g_fwd_variant == 30 || (g_fwd_variant == 0 && D == 128 && DVc == 128))) {
         hipError_t e = hipSuccess;
         if (launch_dense_fwd_p4(p, D, DVc, std::is_same<T, bf16>::value ? FA_DTYPE_BF16 : FA_DTYPE_F16, s, &e)) {
             g_fwd_last_path = 30;
@@ -1056,8 +1059,9 @@ int launch_dense_fwd(const DenseArgs& a, hipStream_t s, const char** why) {
         (int64_t)p.ldk * a.dv * esz >= (int64_t)INT32_MAX)
         p.fast = 0;
     // split-KV for small grids (fast kernels, default geometry, workspace given)
-    // (variant 30: not when fa_fwd_p4's own 256-row blocks already fill the chip)
-    const bool p4_fills = g_fwd_variant == 30 && (a.N + 255) / 256 * a.batch >= device_cus(s);
+    // (not when fa_fwd_p4's own 256-row blocks already fill the chip)
+    const bool p4_fills = (g_fwd_variant == 30 || (g_fwd_variant == 0 && Dc == 128 && DVc == 128)) &&
+                          (a.N + 255) / 256 * a.batch >= device_cus(s);
     if (p.fast && (g_fwd_variant == 0 || g_fwd_variant == 30) && !p4_fills && a.workspace) {
         const SplitPlan sp = split_plan(a.dtype, a.N, a.Nk, a.d, a.dv, a.batch);
         if (sp.nsplit > 1 && a.workspace_bytes >= pad_bytes + sp.bytes) {
