@@ -150,13 +150,23 @@ int fa_debug_set_bwd_mode(int v) {
     return old;
 }
 
-// Not part of the public header: 1 = the single-pass backward hands its running dQ sums
+// Not part of the public header: the single-pass backward hands its running dQ sums
 // over in the XCD's L2 when all of a slab's members run on one XCD (plain stores instead
-// of sc1 write-through); returns the previous value.
+// of sc1 write-through): -1 auto (d, dv <= 64), 0 never, 1 always; returns the previous
+// value (-2 for an invalid argument).
 int fa_debug_set_bwd_l2local(int v) {
     const int old = fa::g_bwd_l2local;
-    if (v < 0 || v > 1) return -1;
+    if (v < -1 || v > 1) return -2;
     fa::g_bwd_l2local = v;
+    return old;
+}
+
+// Not part of the public header: the single-pass backward's step offset between
+// consecutive members of a slice's chain (1..4, default 3); returns the previous value.
+int fa_debug_set_bwd_hoff(int v) {
+    const int old = fa::g_bwd_hoff;
+    if (v < 1 || v > 4) return -1;
+    fa::g_bwd_hoff = v;
     return old;
 }
 

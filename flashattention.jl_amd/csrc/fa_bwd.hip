@@ -1358,7 +1358,9 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
 thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
-thread_local int g_bwd_l2local = 0;         // bwd_fused: L2-local hand-off when a slab sits on one XCD
+thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD
+                                            // (-1 auto: at d, dv <= 64; 0 never; 1 always)
+thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
@@ -1457,7 +1459,7 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
     const int cus = device_cus(s);
-    if (cus < 8 || 3 * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
+    if (cus < 8 || g_bwd_hoff * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
     const int xcd = (K <= cus / 8 && batch % 8 == 0) ? 1 : 0;
     if (g_bwd_mode == 0) {
         // auto: the grid fills the chip, and K divides the CUs a slab's members are dealt
@@ -1580,7 +1582,11 @@ static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStr
     // mode 3 (tests): the timeout word starts set, so every poll gives up and the
     // guarded dQ pass must recompute dQ of every slab
     p.hdr_err = g_bwd_mode == 3 ? 1u : 0u;
-    p.l2local = g_bwd_l2local;
+    // L2-local hand-off: +6 % at d = dv = 64, -1 % at 128, where a slice's running
+    // sums (32 KB) in flight over three steps fill most of the 4-MB L2 that also
+    // serves the slab's Q / dO (profiles/r04_bwd_handoff_modes.log)
+    p.l2local = g_bwd_l2local >= 0 ? g_bwd_l2local : (p.d <= 64 && p.dv <= 64 ? 1 : 0);
+    p.hoff = g_bwd_hoff;
 #ifdef FA_BWD_ABL
     p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode == 10 ? 64
              : g_bwd_mode == 11 ? 64 | 3 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;

@@ -260,6 +260,42 @@ def test_backward_single_pass(fa, N, Nk, d, dv, B, dtype):
         assert_grad_close(_np(a), _np(sp), dtype, nm + " vs split passes")
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_backward_handoff_forms_bitwise(fa, d):
+    """The single pass's two hand-off forms (sc1 write-through, and the XCD-L2-local form
+    used when a slab's members share one XCD: auto at d <= 64) sum dQ in the same order,
+    so dQ, dK, dV are bitwise equal; a chain step offset of 4 instead of 3 reorders the
+    sum (other bits) and still matches the oracle.  Each form on the configs-sized grid
+    (64 slabs) so the single pass and the XCD mapping are the automatic choice."""
+    L = fa.lib()
+    N, BH = 2048, 64
+    g = torch.Generator(device="cuda").manual_seed(31 + d)
+    mk = lambda: fa.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
+    Q, K, V, dO = mk(), mk(), mk(), mk()
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    outs, st = {}, {}
+    old_l2, old_off = L.fa_debug_set_bwd_l2local(-1), L.fa_debug_set_bwd_hoff(3)
+    try:
+        for form in ((0, 3), (1, 3), (-1, 4)):
+            L.fa_debug_set_bwd_l2local(form[0])
+            L.fa_debug_set_bwd_hoff(form[1])
+            outs[form] = [t.clone() for t in fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)]
+            st[form] = fa.backward_handoff_status()
+    finally:
+        L.fa_debug_set_bwd_l2local(old_l2)
+        L.fa_debug_set_bwd_hoff(old_off)
+    assert all(v == 0 for v in st.values()), st
+    for a, b_, nm in zip(outs[(0, 3)], outs[(1, 3)], ("dQ", "dK", "dV")):
+        assert torch.equal(a, b_), nm + ": L2-local hand-off not bitwise equal to sc1"
+    b = 17
+    sl = lambda t: _np(t[:, :, b:b + 1])
+    dqr, dkr, dvr = O.dense_fa_backward(sl(Q), sl(K), sl(V), sl(Oo), sl(dO), _np(l[:, :, b:b + 1]),
+                                        _np(m[:, :, b:b + 1]))
+    for form in outs:
+        for a, r_, nm in zip(outs[form], (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+            assert_grad_close(sl(a), r_, "bfloat16", f"{nm} form {form}")
+
+
 def test_backward_single_pass_fallback(fa):
     """A hand-off timeout (forced: the timeout word starts set) leaves dK, dV of the
     single pass and recomputes dQ in the guarded dQ pass: the result still matches."""
