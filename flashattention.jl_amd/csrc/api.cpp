@@ -170,6 +170,15 @@ int fa_debug_set_bwd_hoff(int v) {
     return old;
 }
 
+// Not part of the public header: the single-pass backward's residency-check window in
+// microseconds (10..20000, default 50); returns the previous value.
+int fa_debug_set_bwd_stall_us(int v) {
+    const int old = fa::g_bwd_stall_us;
+    if (v < 10 || v > 20000) return -1;
+    fa::g_bwd_stall_us = v;
+    return old;
+}
+
 // Not part of the public header: circulant kernel override (1 one-wave-per-query,
 // 2 LDS-tiled SIMT; 0 auto).
 int fa_debug_set_circ_generic(int v) {

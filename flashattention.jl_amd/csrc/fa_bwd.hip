@@ -27,6 +27,8 @@
 
 namespace fa {
 
+constexpr int kStallUs = 50;   // bwd_fused: default window of the residency check (fa_debug_set_bwd_stall_us)
+
 struct BwdParams {
     const void *Q, *K, *V, *O, *dO;
     const float *l, *m;
@@ -46,6 +48,7 @@ struct BwdParams {
     unsigned hdr_plan = 0, hdr_err = 0;
     float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
+    int stall_ticks = kStallUs * 100;   // residency-check window in s_memrealtime ticks (100 MHz)
     int l2local = 0;  // 1: hand the running sums over in the XCD's L2 when a slab's members share one
     int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
@@ -886,7 +889,6 @@ __device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img,
 }
 
 constexpr uint64_t kSpinTicks = 2000000;   // s_memrealtime (100 MHz): 20 ms, the bound of a poll
-constexpr uint64_t kStallTicks = 5000;     // 50 us: the window of the residency check
 
 __device__ __forceinline__ void arrive(gu32* p) {
     __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -902,7 +904,7 @@ __device__ __forceinline__ void arrive(gu32* p) {
 // finishing slabs) keeps arriving, and a complete slab always progresses, so only the
 // 20-ms bound remains for it.
 __device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* arr,
-                                           unsigned members) {
+                                           unsigned members, uint64_t stall_ticks) {
     if (ld_agent(f) >= want) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tw = t0;
@@ -912,7 +914,7 @@ __device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, g
         if (ld_agent(f) >= want || ld_agent(serr) != 0u) return;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         bool trip = now - t0 > kSpinTicks;
-        if (now - tw > kStallTicks) {   // one window over: did the slab grow?
+        if (now - tw > stall_ticks) {   // one window over: did the slab grow?
             const unsigned a = ld_agent(arr);
             trip = trip || (a < members && a == seen);
             seen = a;
@@ -1057,6 +1059,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     gu32* const arr = (gu32*)(p.flags + (int64_t)p.batch * NS + b);               // this slab's arrival count
     gu32* const serr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 1) + b);        // and its trip word
     gu32* const xmask = (gu32*)(p.flags + (int64_t)p.batch * (NS + 2) + b);       // the XCDs of its members
+    const uint64_t stall = (uint64_t)p.stall_ticks;
     if (tid == 0) {
         if (p.l2local) {   // this member's XCD into the slab's mask, acknowledged before it counts as arrived
             const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID[3:0]
@@ -1147,7 +1150,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     bool local = false;
     if (p.l2local) {
         if (tid == 0) {
-            wait_count(arr, (unsigned)KM, serr, err, arr, (unsigned)KM);
+            wait_count(arr, (unsigned)KM, serr, err, arr, (unsigned)KM, stall);
             const unsigned m = ld_agent(xmask);
             s_local = (ld_agent(arr) >= (unsigned)KM && (m & (m - 1u)) == 0u) ? 1u : 0u;
         }
@@ -1175,7 +1178,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         const bool has_tile = NTQ >= 8 || wave < NTQ;
         if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
-        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, serr, err, arr, (unsigned)KM);
+        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, serr, err, arr, (unsigned)KM, stall);
         __syncthreads();
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
@@ -1229,7 +1232,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // and barriers B2 and B1 order it before every wave's sum loads of that step
         if (wave == 0 && i + 1 < NS && !(abl & 1)) {
             const int tn = slice_of(i + 1), pn = chain_pos(tn);
-            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, serr, err, arr, (unsigned)KM);
+            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, serr, err, arr, (unsigned)KM, stall);
         }
         if (has_tile && !(abl & 10)) {
             pin[0] = load16_sc1_asm<0>(pdesc, pofs);
@@ -1361,6 +1364,7 @@ thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single 
 thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD
                                             // (-1 auto: at d, dv <= 64; 0 never; 1 always)
 thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members
+thread_local int g_bwd_stall_us = kStallUs; // bwd_fused: residency-check window
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
@@ -1587,6 +1591,7 @@ static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStr
     // serves the slab's Q / dO (profiles/r04_bwd_handoff_modes.log)
     p.l2local = g_bwd_l2local >= 0 ? g_bwd_l2local : (p.d <= 64 && p.dv <= 64 ? 1 : 0);
     p.hoff = g_bwd_hoff;
+    p.stall_ticks = g_bwd_stall_us * 100;
 #ifdef FA_BWD_ABL
     p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode == 10 ? 64
              : g_bwd_mode == 11 ? 64 | 3 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;

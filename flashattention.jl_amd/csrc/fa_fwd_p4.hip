@@ -64,6 +64,14 @@ constexpr int kP4VS = 2;       // V ring slots (V(t+1) issued in phase B(t))
 #define FA_P4_PF 4
 #endif
 constexpr int kP4Prefetch = FA_P4_PF;   // MFMA slots an LDS operand read runs ahead (LDS latency ~100+ cycles)
+#ifndef FA_P4_DMA
+#define FA_P4_DMA 0
+#endif
+// MFMA slot of DMA piece q of n in a phase of NM slots whose softmax starts at slot np:
+// 0 = back to back from np, 1 = spread evenly over [np, NM), 2 = the last n slots
+__host__ __device__ constexpr int p4_dma_slot(int q, int n, int np, int NM) {
+    return FA_P4_DMA == 1 ? np + q * ((NM - np) / n) : FA_P4_DMA == 2 ? NM - n + q : np + q;
+}
 
 __device__ __forceinline__ uint32_t p4_lds(const void* ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)ptr;
@@ -510,10 +518,12 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         auto side0 = softmax_side(NMt{}, NPt{}, 0, mx0, sm0);
         auto valx = [&](int i) __attribute__((always_inline)) {
             side1(i);
-            // V(j+1) pieces and the Q piece early in the phase
+            // V(j+1) pieces, then the Q piece (slots: p4_dma_slot)
             if (FA_P4_ABL & 1) return;
-            if (i >= NPx && i < NPx + C::VP) dma_v1(vds, vs0 ^ 1, jv2, i - NPx);
-            if (i == NPx + C::VP) {
+#pragma unroll
+            for (int q = 0; q < C::VP; ++q)
+                if (i == p4_dma_slot(q, C::VP + 1, NPx, NMx)) dma_v1(vds, vs0 ^ 1, jv2, q);
+            if (i == p4_dma_slot(C::VP, C::VP + 1, NPx, NMx)) {
                 const bool qv = j < C::QP;
                 dma_q1(p4_desc(qpn, qv ? qnn : 0u), qbn, qv ? j : 0, qv ? qdst(j) : lds0 + C::OOFF + (uint32_t)wave * C::OST);
             }
@@ -529,7 +539,9 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         auto valy = [&](int i) __attribute__((always_inline)) {
             if constexpr (!LAST) {
                 side0(i);
-                if (!(FA_P4_ABL & 1) && i >= NPRE && i < NPRE + C::KP) dma_k1(kds, ks0, jk2, i - NPRE);
+#pragma unroll
+                for (int q = 0; q < C::KP; ++q)
+                    if (!(FA_P4_ABL & 1) && i == p4_dma_slot(q, C::KP, NPRE, NMF)) dma_k1(kds, ks0, jk2, q);
             } else {
                 if (!(FA_P4_ABL & 1) && i < C::KP) dma_k1(kds, ks0, jk2, i);
             }
@@ -543,7 +555,6 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         phase2(std::integral_constant<bool, !LAST>{}, Yes{}, std::integral_constant<int, NPx>{},
                std::integral_constant<int, LAST ? 1000 : NPRE>{}, kslot, vslot, valx, midx, seam, valy, midy);
         if constexpr (!LAST) l_run[0] += sm0.sum();
-        (void)NMx;
         FA_P4_STAMP(5, j);
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::KP) : "memory");
         FA_P4_STAMP(6, j);
