@@ -398,6 +398,15 @@ def _cpu_threads():
     return max(1, n)
 
 
+def _cpu_quota():
+    """The cgroup CPU quota of this process (cpu.max: quota / period), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def _node_cpus():
     """Every host CPU this process may run on (sched_getaffinity): the node's
     cores as north_star's CPU baseline asks for."""
@@ -486,12 +495,14 @@ def cpu_baseline(node: bool = False):
     bl = legs[best]
     return {"value": bl["configs1_fp32_tflops"], "unit": "TFLOP/s", "cores": bl["threads"], "kind": "port",
             "value_from": best, "cpu_model": _cpu_model(), "affinity_cpus": ncpu, "omp_share": share,
+            "cgroup_cpu_quota": _cpu_quota(),
             "sample": f"the whole configs[1] workload (4096,64,64) fp32, C/OpenMP port of dense_fa! "
                       f"(oracle/fa_cpu.c: Br=64 Bc=500 tiles), leg '{best}': {bl['impl']} at {bl['threads']} "
                       f"threads, median of 3: {bl['configs1_s']:.3f} s; 'legs' adds configs[0] and the "
                       f"reference's Float64 case" + ("" if node else
-                      f"; the node-wide legs (all {ncpu} CPUs) run with bench.py --cpu-node "
-                      f"(profiles/r04_cpu_baseline_node.log)"),
+                      f"; the node-wide legs (all {ncpu} affinity CPUs) run with bench.py --cpu-node "
+                      f"(profiles/r04_cpu_baseline_node.log: slower than this leg, since the job's "
+                      f"cgroup quota is {_cpu_quota()} CPUs)"),
             "legs": legs,
             "reference_published": "dense_fa Julia N=512 d=64 bs=1 Float64: 2.392 ms, unstated CPU "
                                    "(/root/reference/logs/compare1.txt:4)"}
