@@ -7,6 +7,7 @@
 // build / run: tools/exp/bwd_strip_stamp.py.
 #include <hip/hip_runtime.h>
 __device__ unsigned long long g_stamp_buf[24 * 16384];
+__device__ unsigned long long g_stamp_ws[256];   // the strip counters' workspace (2 KiB)
 #define FA_BSTAMP(k)                                                                        \
     do {                                                                                   \
         if (threadIdx.x == 0) {                                                            \
@@ -27,6 +28,9 @@ extern "C" int bwd_stamp_run(const void* q, const void* k, const void* v, const 
     a.g.ws = 7; a.g.stride = 7; a.g.pad = 3;
     a.g.O[0] = 19; a.g.O[1] = 19; a.g.O[2] = 1; a.g.T = 49; a.g.L = 361; a.g.P = 128 * 128;
     a.d = 64; a.dv = 64; a.batch = B; a.scale = 0.125f;
+    void* ws = nullptr;
+    if (hipGetSymbolAddress(&ws, HIP_SYMBOL(g_stamp_ws)) != hipSuccess) return 4;
+    a.workspace = ws; a.workspace_bytes = sizeof(unsigned long long) * 256;
     fa::g_win_force_composed = mode;
     const char* why = nullptr;
     int rc = fa::windowed_bwd_rows<fa::bf16>(a, nullptr, &why);
