@@ -45,6 +45,13 @@
 #ifndef FA_P4_STAMP
 #define FA_P4_STAMP(pt, j)
 #endif
+// FA_P4_SLOT(i): a sample of s_memtime at MFMA slot i of a tile's X/Y stream (no wait
+// there); FA_P4_SLOT_FLUSH(j) waits for the samples and records them.
+#ifndef FA_P4_SLOT
+#define FA_P4_SLOT_DECL
+#define FA_P4_SLOT(i)
+#define FA_P4_SLOT_FLUSH(j)
+#endif
 // FA_P4_ABL: timing-only ablations of the diagnostic build (WRONG results): 1 no K/V/Q
 // DMA in the tile loop, 2 no exponentials, 4 no LDS operand reads in the tile loop,
 // 8 no softmax / max VALU work at all, 16 one transposed read per K fragment (of two),
@@ -321,6 +328,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
     f32x16 S[2][2];        // [query block][key block]: one score tile per query block
     u32x4 P[2][2][2];      // [query block][key block][k-step], packed P (dword view of the bf16x8 operand)
     float m_used[2], m_true[2], l_run[2];
+    FA_P4_SLOT_DECL
 
     // ---- one phase: the MFMAs of query block u — Sᵀ_u = K·Qᵀ_u (QK) then Oᵀ_u += Vᵀ·Pᵀ_u
     // (PV) — with valu(slot) after each MFMA and mid() before MFMA slot NPRE.  The LDS
@@ -426,6 +434,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
             }
             if constexpr (u == 0) valx(k);
             else valy(k);
+            FA_P4_SLOT(i);
             p4_fence();
             if constexpr (i == NM - 1) {
                 if constexpr (NPX >= NM) midx();
@@ -555,6 +564,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         phase2(std::integral_constant<bool, !LAST>{}, Yes{}, std::integral_constant<int, NPx>{},
                std::integral_constant<int, LAST ? 1000 : NPRE>{}, kslot, vslot, valx, midx, seam, valy, midy);
         if constexpr (!LAST) l_run[0] += sm0.sum();
+        FA_P4_SLOT_FLUSH(j);
         FA_P4_STAMP(5, j);
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::KP) : "memory");
         FA_P4_STAMP(6, j);

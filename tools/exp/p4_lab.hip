@@ -23,6 +23,22 @@ __device__ unsigned long long g_p4st[256 * 4 * 64];
         }                                                                                             \
     } while (0)
 #endif
+#ifdef P4_SLOTS
+// s_memtime every 4th MFMA slot of the X/Y stream (8 samples per tile at d = 64, 16 at
+// 128), recorded for tile 16 of each workgroup's first block; the wait for the samples
+// is deferred to the end of the stream (no lgkmcnt wait inside it)
+__device__ unsigned long long g_p4slot[256 * 4 * 16];
+#define FA_P4_SLOT_DECL unsigned long long p4ts[16] = {};
+#define FA_P4_SLOT(i)                                                                          \
+    if constexpr ((i) % 4 == 0 && (i) / 4 < 16) asm volatile("s_memtime %0" : "=s"(p4ts[(i) / 4])::"memory");
+#define FA_P4_SLOT_FLUSH(j)                                                                    \
+    do {                                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                     \
+        if ((j) == 16 && p4_blk == 0 && (threadIdx.x & 63) == 0 && blockIdx.x < 256)          \
+            for (int q_ = 0; q_ < 16; ++q_)                                                    \
+                ::g_p4slot[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + q_] = p4ts[q_];         \
+    } while (0)
+#endif
 #include "../../flashattention.jl_amd/csrc/fa_fwd_p4.hip"
 
 extern "C" int p4_launch(int dtype, const void* Q, const void* K, const void* V, void* O, float* l, float* m, int N,
@@ -41,6 +57,12 @@ extern "C" int p4_launch(int dtype, const void* Q, const void* K, const void* V,
     if (!fa::launch_dense_fwd_p4(p, d, d, dtype, (hipStream_t)stream, &e)) return 5;
     return e == hipSuccess ? 0 : 6;
 }
+#ifdef P4_SLOTS
+extern "C" int p4_read_slots(unsigned long long* host_out) {
+    if (hipDeviceSynchronize() != hipSuccess) return 2;
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_p4slot), sizeof(g_p4slot)) == hipSuccess ? 0 : 3;
+}
+#endif
 extern "C" int p4_read(unsigned long long* host_out) {
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_p4st), sizeof(g_p4st)) == hipSuccess ? 0 : 3;
