@@ -330,7 +330,7 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
             "FLOPs = 2.5x forward (the 5 GEMMs bwd_fused executes)"),
         "roofline_fwd_bwd": _mfma_roofline(3.5 * f, t_f + t_b, "forward + backward calls"),
         "bwd_handoff": {-1: "two-pass plan (no hand-off)", 0: "single pass, hand-off completed",
-                        1: "single pass, hand-off TIMED OUT: dQ recomputed by the guarded pass"}.get(hs, hs),
+                        1: "single pass, a slab's hand-off GAVE UP (members not co-resident): its dQ recomputed by the guarded pass"}.get(hs, hs),
         "bwd_handoff_recheck": hs_calls,
         "bwd_fallback_tainted": any(x == 1 for x in hs_calls + [hs]),
     }

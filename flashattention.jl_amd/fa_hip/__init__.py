@@ -392,9 +392,10 @@ def backward_handoff_status(device=None) -> int:
     """fa_dense_bwd_handoff_status for the most recent :func:`dense_fa_backward`
     on the current stream of ``device`` (its workspace is this module's per-stream
     scratch buffer).  Synchronises that stream.  -1: the two-pass form ran (no
-    hand-off); 0: single pass, every dQ hand-off completed; 1: a hand-off timed out
-    and dQ was recomputed by the guarded pass (same values within rounding, other
-    bits, up to ~20 ms slower).  Raises FlashAttentionError when no dense_fa_backward
+    hand-off); 0: single pass, every dQ hand-off completed; 1: some slab's hand-off
+    gave up (its members could not all be resident: no arrival within 50 us, or a
+    20-ms bound) and that slab's dQ was recomputed by the guarded pass (same values
+    within rounding, other bits, slower).  Raises FlashAttentionError when no dense_fa_backward
     has run on this stream, or when another entry point has taken the scratch buffer
     since (the module records the last entry point per (device, stream))."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)

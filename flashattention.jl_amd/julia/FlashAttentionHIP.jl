@@ -73,7 +73,7 @@ end
 
 # dense_fa_backward(Q, K, V, O, dO, l, m) — src/dense.jl:104-167
 # `handoff`: optional Ref{Cint} that receives fa_dense_bwd_handoff_status after the call
-# (-1 two-pass form, 0 single pass completed, 1 a dQ hand-off timed out and dQ was
+# (-1 two-pass form, 0 single pass completed, 1 a slab's dQ hand-off gave up and its dQ was
 # recomputed); it synchronises the stream.
 function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
                            O::ROCArray{T,3}, dO::ROCArray{T,3},

@@ -115,11 +115,12 @@ size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
  * l, m are the forward's outputs.  dQ, dK, dV are fully written, without
  * atomics.  dK and dV are bitwise reproducible.  dQ is bitwise reproducible
  * whenever the single pass's ordered dQ hand-off completes (it sums each query
- * slice over the key blocks in a fixed order); if a hand-off wait times out
- * (20 ms: the members of a slab could not all be resident, e.g. other streams
- * or processes holding CUs), dQ is recomputed by a separate pass that sums in a
- * different order — same values within rounding, not the same bits, and up to
- * ~20 ms slower.  fa_dense_bwd_handoff_status reports which happened. */
+ * slice over the key blocks in a fixed order).  If a slab's hand-off gives up —
+ * its members could not all be resident (other streams or processes holding CUs:
+ * a wait sees no new member arrive within 50 us) or a wait passes 20 ms — dQ of
+ * that slab is recomputed by a separate pass that sums in a different order: same
+ * values within rounding, not the same bits, and slower.
+ * fa_dense_bwd_handoff_status reports whether any slab did. */
 int fa_dense_bwd(int dtype,
                  const void* Q, const void* K, const void* V,
                  const void* O, const void* dO,
@@ -132,8 +133,8 @@ int fa_dense_bwd(int dtype,
 /* Diagnostic for the call that last used `workspace` in fa_dense_bwd: reads the
  * workspace header (synchronises hip_stream, so call it after that backward on the
  * same stream).  *status = -1: that call ran the two-pass form (no hand-off),
- * 0: single pass, every dQ hand-off completed, 1: single pass, a hand-off timed out
- * and dQ was recomputed (see fa_dense_bwd).  FA_ERR_INVALID_ARG if the workspace
+ * 0: single pass, every dQ hand-off completed, 1: single pass, some slab's hand-off
+ * gave up and its dQ was recomputed (see fa_dense_bwd).  FA_ERR_INVALID_ARG if the workspace
  * holds no fa_dense_bwd header. */
 int fa_dense_bwd_handoff_status(const void* workspace, size_t workspace_bytes,
                                 void* hip_stream, int* status);
