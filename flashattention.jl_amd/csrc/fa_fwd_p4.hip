@@ -74,6 +74,13 @@ constexpr int kP4Prefetch = FA_P4_PF;   // MFMA slots an LDS operand read runs a
 #ifndef FA_P4_DMA
 #define FA_P4_DMA 0
 #endif
+#ifndef FA_P4_EARLYMAX
+#define FA_P4_EARLYMAX 0
+#endif
+// 1: a query block's tile maximum runs in the phase that computes its scores (after
+// those MFMAs have retired), so the next phase can spend every MFMA gap on the
+// exponentials (the lazy-rescale decision moves to that phase's first slot)
+constexpr bool kP4EarlyMax = FA_P4_EARLYMAX != 0;
 // MFMA slot of DMA piece q of n in a phase of NM slots whose softmax starts at slot np:
 // 0 = back to back from np, 1 = spread evenly over [np, NM), 2 = the last n slots
 __host__ __device__ constexpr int p4_dma_slot(int q, int n, int np, int NM) {
@@ -485,6 +492,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         };
     };
 
+    float mt1c = 0.0f;   // early max: block 1's tile max for the next X phase
     // per-block DMA context: this block's and the next block's slabs
     int p4_blk = 0;   // block counter of this workgroup (read by the diagnostic stamps only)
     (void)p4_blk;
@@ -497,9 +505,7 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
     constexpr int NMF = C::NKQ + C::NVQ;              // MFMA slots of a full phase
     constexpr int NPRE = NMF >= 32 ? 6 : 4;           // slots carrying the max chains
     typedef std::integral_constant<int, NMF> NMt;
-    typedef std::integral_constant<int, NPRE> NPt;
     typedef std::integral_constant<int, C::NVQ> NMvt;  // PV-only phase (last tile)
-    typedef std::integral_constant<int, (C::NVQ >= 16 ? 4 : 2)> NPvt;
 
     // One tile t (block tile j): X = query block 0's MFMAs ∥ block 1's softmax of tile
     // j; Y = block 1's MFMAs ∥ block 0's softmax of tile j+1.  DMA: the next V tile and
@@ -518,27 +524,40 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         // ---- X: block 0 MFMAs ∥ block 1 softmax (tile j); Y: block 1 MFMAs ∥ block 0
         //      softmax (tile j+1), or on the last tile block 1's PV only ----
         constexpr int NMx = LAST ? C::NVQ : NMF;
-        constexpr int NPx = LAST ? (C::NVQ >= 16 ? 4 : 2) : NPRE;
+        constexpr int NPx = kP4EarlyMax ? 0 : LAST ? (C::NVQ >= 16 ? 4 : 2) : NPRE;   // max slots before the exps
+        constexpr int NPy = kP4EarlyMax ? 0 : NPRE;
+        constexpr int DMx = kP4EarlyMax ? 2 : NPx, DMy = kP4EarlyMax ? 2 : NPRE;     // first DMA slot
+        constexpr int MX0 = C::NKQ + 2;   // early max: first slot after this phase's score MFMAs retired
         MaxQB mx1, mx0;
         SoftmaxQB<T> sm1, sm0;
         sm1.c = c;
         sm0.c = c;
-        auto side1 = softmax_side(std::conditional_t<LAST, NMvt, NMt>{}, std::conditional_t<LAST, NPvt, NPt>{}, 1, mx1, sm1);
-        auto side0 = softmax_side(NMt{}, NPt{}, 0, mx0, sm0);
+        auto side1 = softmax_side(std::conditional_t<LAST, NMvt, NMt>{}, std::integral_constant<int, NPx>{}, 1, mx1, sm1);
+        auto side0 = softmax_side(NMt{}, std::integral_constant<int, NPy>{}, 0, mx0, sm0);
+        // early max of block v's scores computed in this phase (slots MX0 .. NMF-1)
+        auto early_max = [&](int i, int v, MaxQB& mx) __attribute__((always_inline)) {
+            if (FA_P4_ABL & 8) return;
+            if (i >= MX0) {
+#pragma unroll
+                for (int m = MaxQB::NOPS * (i - MX0) / (NMF - MX0); m < MaxQB::NOPS * (i - MX0 + 1) / (NMF - MX0); ++m)
+                    mx.op(S[v], m);
+            }
+        };
         auto valx = [&](int i) __attribute__((always_inline)) {
             side1(i);
+            if constexpr (kP4EarlyMax && !LAST) early_max(i, 0, mx0);
             // V(j+1) pieces, then the Q piece (slots: p4_dma_slot)
             if (FA_P4_ABL & 1) return;
 #pragma unroll
             for (int q = 0; q < C::VP; ++q)
-                if (i == p4_dma_slot(q, C::VP + 1, NPx, NMx)) dma_v1(vds, vs0 ^ 1, jv2, q);
-            if (i == p4_dma_slot(C::VP, C::VP + 1, NPx, NMx)) {
+                if (i == p4_dma_slot(q, C::VP + 1, DMx, NMx)) dma_v1(vds, vs0 ^ 1, jv2, q);
+            if (i == p4_dma_slot(C::VP, C::VP + 1, DMx, NMx)) {
                 const bool qv = j < C::QP;
                 dma_q1(p4_desc(qpn, qv ? qnn : 0u), qbn, qv ? j : 0, qv ? qdst(j) : lds0 + C::OOFF + (uint32_t)wave * C::OST);
             }
         };
         auto midx = [&]() __attribute__((always_inline)) {
-            decide(1, mx1.mt);
+            decide(1, kP4EarlyMax ? mt1c : mx1.mt);
             sm1.nmc = -m_used[1] * c;
         };
         auto seam = [&]() __attribute__((always_inline)) {
@@ -548,9 +567,10 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
         auto valy = [&](int i) __attribute__((always_inline)) {
             if constexpr (!LAST) {
                 side0(i);
+                if constexpr (kP4EarlyMax) early_max(i, 1, mx1);
 #pragma unroll
                 for (int q = 0; q < C::KP; ++q)
-                    if (!(FA_P4_ABL & 1) && i == p4_dma_slot(q, C::KP, NPRE, NMF)) dma_k1(kds, ks0, jk2, q);
+                    if (!(FA_P4_ABL & 1) && i == p4_dma_slot(q, C::KP, DMy, NMF)) dma_k1(kds, ks0, jk2, q);
             } else {
                 if (!(FA_P4_ABL & 1) && i < C::KP) dma_k1(kds, ks0, jk2, i);
             }
@@ -562,8 +582,9 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
             }
         };
         phase2(std::integral_constant<bool, !LAST>{}, Yes{}, std::integral_constant<int, NPx>{},
-               std::integral_constant<int, LAST ? 1000 : NPRE>{}, kslot, vslot, valx, midx, seam, valy, midy);
+               std::integral_constant<int, LAST ? 1000 : NPy>{}, kslot, vslot, valx, midx, seam, valy, midy);
         if constexpr (!LAST) l_run[0] += sm0.sum();
+        if constexpr (kP4EarlyMax && !LAST) mt1c = mx1.mt;
         FA_P4_SLOT_FLUSH(j);
         FA_P4_STAMP(5, j);
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::KP) : "memory");
@@ -643,6 +664,12 @@ __global__ __launch_bounds__(256, 1) void dense_fwd_p4(FwdParams p) {
 #pragma unroll
             for (int part = 0; part < 32; ++part) sm.part(S[0], P[0], part);
             l_run[0] += sm.sum();
+            if constexpr (kP4EarlyMax) {   // block 1's tile-0 max for the first X phase
+                MaxQB mx1;
+#pragma unroll
+                for (int m = 0; m < MaxQB::NOPS; ++m) mx1.op(S[1], m);
+                mt1c = (FA_P4_ABL & 8) ? 0.0f : mx1.mt;
+            }
         }
         FA_P4_STAMP(1, -1);
 

@@ -40,6 +40,14 @@ for rnd in range(6):
             f()
         e1.record(); torch.cuda.synchronize()
         times[k].append(e0.elapsed_time(e1) / 10 * 1e3)
+ref = None
+same = {}
+for k, f in fns.items():   # bitwise check of each build's O against the default kernel's
+    f(); torch.cuda.synchronize()
+    if ref is None:
+        ref = O.clone()
+    same[k] = bool(torch.equal(O.view(torch.int16), ref.view(torch.int16)))
 for k, ts in times.items():
     us = float(np.median(ts))
-    print(f"N={N} d={d} BH={BH} {k}: {us:.1f} us  {flops / us / 1e6:.0f} TFLOP/s", flush=True)
+    print(f"N={N} d={d} BH={BH} {k}: {us:.1f} us  {flops / us / 1e6:.0f} TFLOP/s  O bitwise equal to v0: {same[k]}",
+          flush=True)
