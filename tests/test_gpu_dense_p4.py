@@ -54,6 +54,7 @@ SHAPES = [
     (512, 1152, 128, 128, "bfloat16"),   # d = 128: 256 blocks, 18 key tiles (Q prefetch needs 17)
     (768, 1088, 128, 96, "float16"),     # f16, 288 blocks
     (4096, 4096, 64, 16, "float16"),     # f16, 256 blocks of 64 tiles
+    (1000, 1088, 128, 256, "bfloat16"),  # d = 128, partial last block, 1024 blocks (4 per workgroup)
 ]
 
 
@@ -126,3 +127,17 @@ def test_p4_falls_back_outside_its_rules(fa):
         assert path30 == 0, (N, Nk, d, B)
         y0, l0, m0, _ = _run(fa, 0, Q, K, V)
         assert torch.equal(y30, y0) and torch.equal(l30, l0) and torch.equal(m30, m0)
+
+
+def test_p4_is_the_d128_default(fa):
+    """At d = dv = 128 the default forward (variant 0) runs fa_fwd_p4 on eligible shapes
+    and equals the 8-wave kernel (variant 5) bitwise; at d = 64 the default stays the
+    8-wave kernel."""
+    rng = np.random.default_rng(77)
+    for (N, d, B, want) in ((2048, 128, 64, 30), (2048, 64, 64, 0)):
+        Q, K, V = (fa.jl_tensor(rng.standard_normal((N, d, B)), torch.bfloat16) for _ in range(3))
+        y0, l0, m0, path0 = _run(fa, 0, Q, K, V)
+        assert path0 == want, (d, path0)
+        y5, l5, m5, _ = _run(fa, 5 if d == 128 else 7, Q, K, V)
+        assert torch.equal(y0.view(torch.int16), y5.view(torch.int16))
+        assert torch.equal(l0, l5) and torch.equal(m0, m5)
