@@ -855,8 +855,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // vmcnt(0) of a step is the one in the middle of phase A.
 // Every member of a slab must be resident at once: dispatch order within an XCD
 // is monotone, so a slab's members are dealt either to one XCD (K <= 32) or across
-// all of them.  A poll gives up when its slab is missing members and no more arrive
-// within 50 us (a co-tenant holds the CUs: see wait_count), or after 20 ms; it then
+// all of them.  A poll gives up when its slab is missing members while the launch
+// dispatches no workgroup for 50 us (a co-tenant holds the CUs: see wait_count), or
+// after 20 ms; it then
 // sets the slab's trip word and the call's status word `err`; the slab's other polls
 // stop at once, and the guarded bwd_dq_fast that follows recomputes dQ of the slabs
 // that tripped (dK, dV do not depend on the hand-off).
@@ -896,28 +897,31 @@ __device__ __forceinline__ void arrive(gu32* p) {
 
 // One lane waits until *f >= want, or gives up: then the slab's trip word *serr and
 // the call's status word *herr are set, and the slab's other polls stop.  Residency
-// check: every member of the slab adds 1 to *arr when it starts, so while a member is
-// missing the chain may wait on a workgroup that cannot be dispatched until resident
-// ones finish (another process holds CUs).  A poll that has waited one 50-us window
-// trips at once if the slab is still incomplete and no member arrived during that
-// window; a slab whose members are still being dispatched (a second wave behind
-// finishing slabs) keeps arriving, and a complete slab always progresses, so only the
-// 20-ms bound remains for it.
+// check: every member adds 1 to its slab's arrival count *arr and to the launch's
+// *garr when it starts.  While a member of the slab is missing, the chain may wait on
+// a workgroup that cannot be dispatched until resident ones finish.  If this launch
+// still dispatches workgroups somewhere (*garr grows), the missing member is queued
+// behind this launch's own running slabs, which always progress (in-order dispatch:
+// a partial slab is at the dispatch frontier; the lowest frontier's slabs are
+// complete), so the poll keeps waiting.  A window of stall_ticks (50 us) with the slab
+// incomplete and no workgroup of the launch arriving anywhere means every resident
+// workgroup waits on CUs another process or stream holds: the poll trips.  A complete
+// slab always progresses, so for it only the 20-ms bound remains.
 __device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* arr,
-                                           unsigned members, uint64_t stall_ticks) {
+                                           gu32* garr, unsigned members, uint64_t stall_ticks) {
     if (ld_agent(f) >= want) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tw = t0;
-    unsigned seen = ld_agent(arr);
+    unsigned seen = ld_agent(garr);
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         if (ld_agent(f) >= want || ld_agent(serr) != 0u) return;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         bool trip = now - t0 > kSpinTicks;
-        if (now - tw > stall_ticks) {   // one window over: did the slab grow?
-            const unsigned a = ld_agent(arr);
-            trip = trip || (a < members && a == seen);
-            seen = a;
+        if (now - tw > stall_ticks) {   // one window over: slab incomplete, launch not dispatching?
+            const unsigned ga = ld_agent(garr);
+            trip = trip || (ld_agent(arr) < members && ga == seen);
+            seen = ga;
             tw = now;
         }
         if (trip) {
@@ -1059,6 +1063,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     gu32* const arr = (gu32*)(p.flags + (int64_t)p.batch * NS + b);               // this slab's arrival count
     gu32* const serr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 1) + b);        // and its trip word
     gu32* const xmask = (gu32*)(p.flags + (int64_t)p.batch * (NS + 2) + b);       // the XCDs of its members
+    gu32* const garr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 3));            // the launch's arrival count
     const uint64_t stall = (uint64_t)p.stall_ticks;
     if (tid == 0) {
         if (p.l2local) {   // this member's XCD into the slab's mask, acknowledged before it counts as arrived
@@ -1067,6 +1072,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         arrive(arr);
+        arrive(garr);
     }
 
     const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
@@ -1150,7 +1156,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     bool local = false;
     if (p.l2local) {
         if (tid == 0) {
-            wait_count(arr, (unsigned)KM, serr, err, arr, (unsigned)KM, stall);
+            wait_count(arr, (unsigned)KM, serr, err, arr, garr, (unsigned)KM, stall);
             const unsigned m = ld_agent(xmask);
             s_local = (ld_agent(arr) >= (unsigned)KM && (m & (m - 1u)) == 0u) ? 1u : 0u;
         }
@@ -1178,7 +1184,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         const bool has_tile = NTQ >= 8 || wave < NTQ;
         if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
-        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, serr, err, arr, (unsigned)KM, stall);
+        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, serr, err, arr, garr, (unsigned)KM, stall);
         __syncthreads();
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
@@ -1232,7 +1238,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // and barriers B2 and B1 order it before every wave's sum loads of that step
         if (wave == 0 && i + 1 < NS && !(abl & 1)) {
             const int tn = slice_of(i + 1), pn = chain_pos(tn);
-            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, serr, err, arr, (unsigned)KM, stall);
+            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, serr, err, arr, garr, (unsigned)KM, stall);
         }
         if (has_tile && !(abl & 10)) {
             pin[0] = load16_sc1_asm<0>(pdesc, pofs);
@@ -1474,7 +1480,8 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     f.nkb = (int)K;
     f.nqt = (int)T;
     f.xcd = xcd;
-    f.flag_bytes = al256((size_t)(batch * T + 3 * batch) * 4);   // slice counters; slab arrivals, trip words, XCD masks
+    f.flag_bytes = al256((size_t)(batch * T + 3 * batch + 1) * 4);   // slice counters; slab arrivals, trip words,
+                                                                    // XCD masks; the launch's arrival count
     f.bytes = f.flag_bytes + al256((size_t)(batch * T * (d / 16)) * 4096) + 256;
     return f;
 }
