@@ -161,6 +161,16 @@ int fa_debug_set_bwd_l2local(int v) {
     return old;
 }
 
+// Not part of the public header: the single-pass backward's slab placement: -1 auto (a
+// slab's members on one XCD when they fit), 0 members dealt over the whole chip;
+// returns the previous value (-2 for an invalid argument).
+int fa_debug_set_bwd_xcd(int v) {
+    const int old = fa::g_bwd_xcd;
+    if (v < -1 || v > 0) return -2;
+    fa::g_bwd_xcd = v;
+    return old;
+}
+
 // Not part of the public header: the single-pass backward's step offset between
 // consecutive members of a slice's chain (1..4, default 3); returns the previous value.
 int fa_debug_set_bwd_hoff(int v) {

@@ -1371,6 +1371,7 @@ thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when
                                             // (-1 auto: at d, dv <= 64; 0 never; 1 always)
 thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members
 thread_local int g_bwd_stall_us = kStallUs; // bwd_fused: residency-check window
+thread_local int g_bwd_xcd = -1;            // bwd_fused: one XCD per slab where eligible (-1 auto, 0 never)
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
@@ -1470,7 +1471,7 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
     const int cus = device_cus(s);
     if (cus < 8 || g_bwd_hoff * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
-    const int xcd = (K <= cus / 8 && batch % 8 == 0) ? 1 : 0;
+    const int xcd = (K <= cus / 8 && batch % 8 == 0 && g_bwd_xcd != 0) ? 1 : 0;
     if (g_bwd_mode == 0) {
         // auto: the grid fills the chip, and K divides the CUs a slab's members are dealt
         // over (one XCD's, or the chip's), so no slab waits part-resident behind another
