@@ -293,7 +293,7 @@ def _mfma_roofline(flops, seconds, kernel, note=None):
     return r
 
 
-def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
+def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5, split=False):
     """BASELINE configs[3]: dense_fa bf16 (B,H,N,d) = (4,16,8192,128) forward,
     backward (reference src/dense.jl:104-167, executable spec
     src_cpp/FlashAttention.cpp:194-252) and forward+backward.  FLOPs: forward
@@ -325,9 +325,10 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
         "fwd_ms": t_f * 1e3, "bwd_ms": t_b * 1e3, "steps_fwd": steps_fwd, "steps_bwd": steps_bwd,
         "roofline_fwd": _mfma_roofline(f, t_f, k_f),
         "roofline_bwd": _mfma_roofline(
-            2.5 * f, t_b, "fa::bwd_fused<bf16,128,128>",
-            "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + bwd_fused + the guarded dQ pass), "
-            "FLOPs = 2.5x forward (the 5 GEMMs bwd_fused executes)"),
+            2.5 * f, t_b, "fa::bwd_dkdv_fast + fa::bwd_dq_fast" if split else "fa::bwd_fused<bf16,128,128>",
+            "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + " +
+            ("the split dK/dV and dQ passes), " if split else "bwd_fused + the guarded dQ pass), ") +
+            "FLOPs = 2.5x forward (the 5 GEMMs of the single pass)"),
         "roofline_fwd_bwd": _mfma_roofline(3.5 * f, t_f + t_b, "forward + backward calls"),
         "bwd_handoff": {-1: "two-pass plan (no hand-off)", 0: "single pass, hand-off completed",
                         1: "single pass, a slab's hand-off GAVE UP (members not co-resident): its dQ recomputed by the guarded pass"}.get(hs, hs),
@@ -580,6 +581,9 @@ def main():
         print("bench.py: FA_BENCH_CPU_STEP is a CPU test hook; refusing it on a GPU box", file=sys.stderr)
         return 2
     dist, rank, world, local = dist_init("gloo" if cpu_hook else None)
+    # the one-GPU rehearsal (FA_BENCH_BACKEND=gloo): every rank on cuda:0
+    shared_gpu = (not cpu_hook and world > 1 and os.environ.get("FA_BENCH_BACKEND") == "gloo"
+                  and torch.cuda.is_available())
 
     if cpu_hook:
         fa_hip = None
@@ -588,6 +592,12 @@ def main():
     else:
         import fa_hip
         fa_hip.lib()
+        if shared_gpu:
+            # co-tenant ranks: the single-pass backward needs every member of a slab
+            # resident at once, which another process's kernels on the same CUs defeat
+            # (it trips and recomputes dQ: 16-18 ms per configs[3] call against 14.1 for
+            # the split passes, profiles/r04_bwd_two_process_placement.log)
+            fa_hip.lib().fa_debug_set_bwd_mode(1)
         BH = B_ * H_
         gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
         Q = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
@@ -639,7 +649,9 @@ def main():
         out["cpu_step_hook"] = True
 
     if not args.no_cfg23 and not cpu_hook:
-        out["cfg3"] = cfg3_block(fa_hip, dist)
+        out["cfg3"] = cfg3_block(fa_hip, dist, split=shared_gpu)
+        if shared_gpu:
+            out["cfg3"]["bwd_plan"] = "split passes: the ranks share one GPU"
         out["cfg2"] = cfg2_block(fa_hip, dist)
     if not args.no_cfg4:
         out["cfg4"] = cfg4_block(fa_hip, world, rank, dist, args.cfg4_steps, 1, cpu_hook)

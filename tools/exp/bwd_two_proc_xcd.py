@@ -1,6 +1,7 @@
 """Two processes on one GPU, each timing configs[3]'s backward (8192, 128, 64 bf16), with
 the single pass's slabs on one XCD each (auto) or dealt over the chip
-(fa_debug_set_bwd_xcd(0)); plus the solo figures.  The parent never touches the GPU:
+(fa_debug_set_bwd_xcd(0)), and the split passes (9: fa_debug_set_bwd_mode(1)); plus the
+solo figures.  The parent never touches the GPU:
 it starts workers with Popen.
 Usage: python tools/exp/bwd_two_proc_xcd.py"""
 import os, subprocess, sys, time
@@ -11,7 +12,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "--worker":
     sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
     import torch, fa_hip
     L = fa_hip.lib()
-    L.fa_debug_set_bwd_xcd(xcd)
+    if xcd == 9:
+        L.fa_debug_set_bwd_mode(1)   # the split passes (no hand-off)
+    else:
+        L.fa_debug_set_bwd_xcd(xcd)
     g = torch.Generator(device="cuda").manual_seed(os.getpid() % 1000)
     N, d, BH = 8192, 128, 64
     mk = lambda: fa_hip.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
@@ -43,6 +47,6 @@ def run(nproc, xcd, reps=5):
 
 
 for rnd in range(1):
-    for xcd in (-1, 0):
+    for xcd in (-1, 0, 9):
         print(f"xcd {xcd}: solo per-call ms and last statuses: {run(1, xcd)}", flush=True)
         print(f"xcd {xcd}: two processes: {run(2, xcd)}", flush=True)

@@ -5,7 +5,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
 cd $R
-timeout -k 10 330 python -u tools/exp/bwd_two_proc_xcd.py > $O/bwd_two_proc_xcd.log 2>&1 || { echo "xcd a/b failed"; exit 9; }
+timeout -k 10 420 python -u tools/exp/bwd_two_proc_xcd.py > $O/bwd_two_proc_xcd.log 2>&1 || { echo "xcd a/b failed"; exit 9; }
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread > $O/final_pytest_gpu.log 2>&1 || { echo "pytest failed"; exit 1; }
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')" > $O/final_smoke.log 2>&1 || { echo "smoke failed"; exit 2; }
 timeout -k 10 300 python -u bench.py > $O/final_bench.log 2>&1 || { echo "bench failed"; exit 3; }
