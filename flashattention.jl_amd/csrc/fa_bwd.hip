@@ -18,6 +18,7 @@
 // Two implementations: the MFMA fast path (bf16/fp16, aligned, Nk % 8 == 0,
 // N % 8 == 0) and a generic LDS-tiled SIMT path (fp32, ragged or unaligned
 // shapes) used for parity on every dtype.
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -1366,7 +1367,17 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 }
 
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
-thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
+// FA_HIP_BWD_SPLIT=1 in the environment selects the split passes for every call:
+// processes that share one GPU should, since the single pass needs every member of a
+// slab resident at once and a co-tenant's kernels hold the CUs it needs.
+static int env_bwd_mode() {
+    static const int m = [] {
+        const char* e = std::getenv("FA_HIP_BWD_SPLIT");
+        return (e != nullptr && e[0] == '1' && e[1] == '\0') ? 1 : 0;
+    }();
+    return m;
+}
+thread_local int g_bwd_mode = env_bwd_mode();   // 0 auto, 1 split passes, 2 single pass where the shape allows
 thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD
                                             // (-1 auto: at d, dv <= 64; 0 never; 1 always)
 thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members
