@@ -365,7 +365,9 @@ def fused_softmax(S: torch.Tensor, dims: int = 1) -> torch.Tensor:
 
 def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
     """``dense_fa_backward(Q, K, V, O, dO, l, m) -> (dQ, dK, dV)`` —
-    src/dense.jl:104-167 (executable spec src_cpp/FlashAttention.cpp:194-252)."""
+    src/dense.jl:104-167 (executable spec src_cpp/FlashAttention.cpp:194-252).
+    Processes that share one GPU should set ``FA_HIP_BWD_SPLIT=1`` before the library
+    loads: the single pass needs every member of a slab resident at once."""
     for t in (Q, K, V, O, dO, l, m):
         _require(t.dim() == 3, "dense_fa_backward expects 3-D (N, d, batch) arrays")
     N, d, B = Q.shape
