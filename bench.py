@@ -590,14 +590,15 @@ def main():
         step = _cpu_hook_step(rank)
         sync, events = (lambda: None), False
     else:
-        import fa_hip
-        fa_hip.lib()
         if shared_gpu:
             # co-tenant ranks: the single-pass backward needs every member of a slab
             # resident at once, which another process's kernels on the same CUs defeat
             # (it trips and recomputes dQ: 16-18 ms per configs[3] call against 14.1 for
-            # the split passes, profiles/r04_bwd_two_process_placement.log)
-            fa_hip.lib().fa_debug_set_bwd_mode(1)
+            # the split passes, profiles/r04_bwd_two_process_placement.log); the
+            # deployment switch, read when the library loads
+            os.environ["FA_HIP_BWD_SPLIT"] = "1"
+        import fa_hip
+        fa_hip.lib()
         BH = B_ * H_
         gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
         Q = _randn_jl(fa_hip, (N_, D_, BH), torch.bfloat16, gen)
