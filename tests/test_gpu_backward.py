@@ -263,8 +263,10 @@ def test_backward_single_pass(fa, N, Nk, d, dv, B, dtype):
 @pytest.mark.parametrize("d", [64, 128])
 def test_backward_handoff_forms_bitwise(fa, d):
     """The single pass's two hand-off forms (sc1 write-through, and the XCD-L2-local form
-    used when a slab's members share one XCD: auto at d <= 64) sum dQ in the same order,
-    so dQ, dK, dV are bitwise equal; a chain step offset of 4 instead of 3 reorders the
+    used when a slab's members share one XCD: auto at d <= 64) and the two slab
+    placements (one XCD per slab, or members dealt over the chip, where the L2-local
+    form does not apply) sum dQ in the same order, so dQ, dK, dV are bitwise equal;
+    a chain step offset of 4 instead of 3 reorders the
     sum (other bits) and still matches the oracle.  Each form on the configs-sized grid
     (64 slabs) so the single pass and the XCD mapping are the automatic choice."""
     L = fa.lib()
@@ -274,19 +276,23 @@ def test_backward_handoff_forms_bitwise(fa, d):
     Q, K, V, dO = mk(), mk(), mk(), mk()
     Oo, l, m = fa.dense_fa(Q, K, V)
     outs, st = {}, {}
-    old_l2, old_off = L.fa_debug_set_bwd_l2local(-1), L.fa_debug_set_bwd_hoff(3)
+    old_l2, old_off, old_x = L.fa_debug_set_bwd_l2local(-1), L.fa_debug_set_bwd_hoff(3), L.fa_debug_set_bwd_xcd(-1)
     try:
-        for form in ((0, 3), (1, 3), (-1, 4)):
+        # (L2-local form, step offset, slab placement: -1 one XCD per slab, 0 chip-wide)
+        for form in ((0, 3, -1), (1, 3, -1), (-1, 4, -1), (-1, 3, 0)):
             L.fa_debug_set_bwd_l2local(form[0])
             L.fa_debug_set_bwd_hoff(form[1])
+            L.fa_debug_set_bwd_xcd(form[2])
             outs[form] = [t.clone() for t in fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)]
             st[form] = fa.backward_handoff_status()
     finally:
         L.fa_debug_set_bwd_l2local(old_l2)
         L.fa_debug_set_bwd_hoff(old_off)
+        L.fa_debug_set_bwd_xcd(old_x)
     assert all(v == 0 for v in st.values()), st
-    for a, b_, nm in zip(outs[(0, 3)], outs[(1, 3)], ("dQ", "dK", "dV")):
+    for a, b_, c_, nm in zip(outs[(0, 3, -1)], outs[(1, 3, -1)], outs[(-1, 3, 0)], ("dQ", "dK", "dV")):
         assert torch.equal(a, b_), nm + ": L2-local hand-off not bitwise equal to sc1"
+        assert torch.equal(a, c_), nm + ": members dealt chip-wide not bitwise equal to one XCD per slab"
     b = 17
     sl = lambda t: _np(t[:, :, b:b + 1])
     dqr, dkr, dvr = O.dense_fa_backward(sl(Q), sl(K), sl(V), sl(Oo), sl(dO), _np(l[:, :, b:b + 1]),
