@@ -34,6 +34,27 @@ end
 
 stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
 
+# Scratch for the C ABI's workspace arguments: ONE buffer per (device, stream), grown on
+# demand and reused, as the Python mirror's _workspace (fa_hip/__init__.py).  Calls on
+# one stream run in order, so reusing the buffer across calls is safe; calls on
+# different streams never share one.  A replaced buffer is freed stream-ordered on the
+# stream that used it.  (Without this cache every backward call allocated its
+# workspace: 268 MB at configs[3], 8.6 GB at configs[4].)
+const _WS = Dict{Tuple{Int,UInt},ROCArray{UInt8,1}}()
+const _WS_LOCK = ReentrantLock()
+function workspace(nbytes::Integer)
+    key = (AMDGPU.device_id(AMDGPU.device()), UInt(stream_ptr()))
+    lock(_WS_LOCK) do
+        buf = get(_WS, key, nothing)
+        if buf === nothing || length(buf) < max(Int(nbytes), 1)
+            buf === nothing || AMDGPU.unsafe_free!(buf)
+            buf = ROCArray{UInt8}(undef, max(Int(nbytes), 1))
+            _WS[key] = buf
+        end
+        buf
+    end
+end
+
 # dense_fa!(O, l, m, Q, K, V) — replaces the body of src/dense.jl:21-102
 function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
                    Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T}
@@ -50,12 +71,27 @@ function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32
                         Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
                        fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, stream_ptr()))
     else   # ragged Nk: zero-padded K / V copies in the workspace let the fast kernels run
-        ws = ROCArray{UInt8}(undef, Int(nws))
+        ws = workspace(nws)
         fa_check(ccall((:fa_dense_fwd_ws, libfa_hip), Cint,
                        (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
                         Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
                        fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, ws, nws, stream_ptr()))
     end
+    return O, l, m
+end
+
+# l, m in any other element type — what the reference's own wrapper allocates,
+# `l = similar(Q, N, 1, B)` (src/dense.jl:12-13), i.e. T itself for Float64, Float16 and
+# BFloat16 inputs.  The C ABI writes float32 statistics: they are staged in Float32 and
+# converted on the device (for Float64 the kernels keep l, m in double internally and
+# round them to Float32 at this boundary, DESIGN.md §3).
+function dense_fa!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
+                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T,S}
+    size(l) == size(m) || throw(DimensionMismatch("l, m"))
+    lf, mf = similar(l, Float32), similar(m, Float32)
+    dense_fa!(O, lf, mf, Q, K, V)
+    l .= lf
+    m .= mf
     return O, l, m
 end
 
@@ -90,7 +126,7 @@ function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
     dQ, dK, dV = similar(Q), similar(K), similar(V)
     nws = ccall((:fa_dense_bwd_workspace, libfa_hip), Csize_t,
                 (Cint, Int64, Int64, Int64, Int64, Int64), fa_dtype(T), N, Nk, d, dv, B)
-    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    ws = workspace(nws)
     fa_check(ccall((:fa_dense_bwd, libfa_hip), Cint,
                    (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32},
                     Ptr{Float32}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
@@ -102,6 +138,14 @@ function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
                        (Ptr{Cvoid}, Csize_t, Ptr{Cvoid}, Ptr{Cint}), ws, nws, stream_ptr(), handoff))
     end
     return dQ, dK, dV
+end
+
+# the backward with l, m in the caller's element type (from the dense_fa! method above)
+function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
+                           O::ROCArray{T,3}, dO::ROCArray{T,3},
+                           l::ROCArray{S,3}, m::ROCArray{S,3};
+                           handoff::Union{Nothing,Base.RefValue{Cint}}=nothing) where {T,S}
+    return dense_fa_backward(Q, K, V, O, dO, Float32.(l), Float32.(m); handoff=handoff)
 end
 
 # windowed_fa(q, k, v, ws; stride, pad) — src/windowed.jl:3-23 (fused on the device)
@@ -117,7 +161,7 @@ function windowed_fa(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,N}, windo
     nws = ccall((:fa_windowed_fwd_workspace, libfa_hip), Csize_t,
                 (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),
                 fa_dtype(T), nsp, spatial, d, dv, B, windowsize, stride, pad)
-    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    ws = workspace(nws)
     fa_check(ccall((:fa_windowed_fwd, libfa_hip), Cint,
                    (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
                     Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64, Cfloat,
@@ -148,7 +192,7 @@ function windowed_fa_backward(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,
     nws = ccall((:fa_windowed_workspace, libfa_hip), Csize_t,
                 (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),
                 fa_dtype(T), nsp, spatial, d, dv, B, windowsize, stride, pad)
-    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    ws = workspace(nws)
     fa_check(ccall((:fa_windowed_bwd, libfa_hip), Cint,
                    (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
                     Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64,
@@ -205,6 +249,17 @@ function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Flo
     return O, l, m
 end
 
+# circulant_fa! with l, m in the caller's element type (staged in Float32, as dense_fa!)
+function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
+                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T,S}
+    size(l) == size(m) || throw(DimensionMismatch("l, m"))
+    lf, mf = similar(l, Float32), similar(m, Float32)
+    circulant_fa!(O, lf, mf, Q, K, V, W)
+    l .= lf
+    m .= mf
+    return O, l, m
+end
+
 # circulant_fa(Q, K, V, W) — src/circulant.jl:1-7, passing W (the reference call drops it)
 function circulant_fa(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
     N, _, B = size(Q)
@@ -221,7 +276,7 @@ function fused_softmax!(P::ROCArray{T,3}, S::ROCArray{T,3}; dims=1) where {T}
     size(P) == size(S) || throw(DimensionMismatch("P and S must have the same size"))
     M, N, B = size(S)
     nws = ccall((:fa_softmax_workspace, libfa_hip), Csize_t, (Int64, Int64, Int64, Cint), M, N, B, dims)
-    ws = ROCArray{UInt8}(undef, max(Int(nws), 1))
+    ws = workspace(nws)
     fa_check(ccall((:fa_softmax, libfa_hip), Cint,
                    (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Int64, Cint, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
                    fa_dtype(T), S, P, M, N, B, dims, ws, nws, stream_ptr()))
