@@ -28,7 +28,32 @@
 
 namespace fa {
 
-constexpr int kStallUs = 50;   // bwd_fused: default window of the residency check (fa_debug_set_bwd_stall_us)
+// bwd_fused: a poll gives up only when the whole launch has published nothing for this
+// long (fa_debug_set_bwd_stall_us): a safety net, not a scheduling decision (§ bwd_fused)
+constexpr int kStallUs = 100000;
+
+// Single-pass hand-off words in the workspace (zeroed per call), in 32-bit words from
+// BwdParams::flags, for `batch` slabs of NS slices and KM members:
+struct FusedFlags {
+    int64_t cnt;    // [2 chains][batch][NS]: members of the chain that have published slice t
+    int64_t fin;    // [batch][NS]: tails of a wrapped slice's two chains that stored their sums
+    int64_t serr;   // [batch]: the slab gave up (its dQ is recomputed by bwd_dq_fast)
+    int64_t xcc;    // [batch][KM]: XCD of each member + 1 (L2-local hand-off)
+    int64_t garr;   // the launch's progress count (arrivals and publishes)
+    int64_t comb;   // a wrapped slice is left to bwd_dq_fast's combine
+    int64_t words;
+};
+__host__ __device__ inline FusedFlags fused_flags(int64_t batch, int64_t NS, int64_t KM) {
+    FusedFlags f;
+    f.cnt = 0;
+    f.fin = 2 * batch * NS;
+    f.serr = 3 * batch * NS;
+    f.xcc = f.serr + batch;
+    f.garr = f.xcc + batch * KM;
+    f.comb = f.garr + 1;
+    f.words = f.comb + 1;
+    return f;
+}
 
 struct BwdParams {
     const void *Q, *K, *V, *O, *dO;
@@ -41,19 +66,21 @@ struct BwdParams {
     float scale, scale_log2;
     double scale64 = 0.0;        // Float64 generic path: τ in double
     // single-pass kernel (bwd_fused): dQ hand-off state, all in the caller's workspace
-    unsigned* flags = nullptr;   // [batch][nqt] members that have published slice t (zeroed per call)
+    unsigned* flags = nullptr;   // hand-off words (FusedFlags, zeroed per call)
     unsigned* err = nullptr;     // hand-off timeout word = hdr[1] (set per call by the pre-pass)
     // workspace header (first 256 B of the aligned workspace; fa_dense_bwd_handoff_status):
     // hdr[0] = kBwdHdrMagic | plan (1 = single pass), hdr[1] = the timeout word
     unsigned* hdr = nullptr;
     unsigned hdr_plan = 0, hdr_err = 0;
-    float* part = nullptr;       // [batch][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
+    float* part = nullptr;       // [batch][2 chains][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
-    int stall_ticks = kStallUs * 100;   // residency-check window in s_memrealtime ticks (100 MHz)
+    int stall_ticks = kStallUs * 100;   // no-progress bound of a poll in s_memrealtime ticks (100 MHz)
     int l2local = 0;  // 1: hand the running sums over in the XCD's L2 when a slab's members share one
     int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
     const unsigned* sguard = nullptr;          // ... and then only on the slabs b with sguard[b] != 0
+    const unsigned* cguard = nullptr;          // bwd_dq_fast: combine the wrapped slices bwd_fused left (*cguard != 0)
+    const unsigned* fin = nullptr;             // ... those with fin[b][t] == 2
 };
 
 template <class T> __device__ __forceinline__ float to_f(T x) { return (float)x; }
@@ -557,17 +584,60 @@ struct FragAddr {
     int row[2];     // [h-independent] b128 row read: swizzled chunk offsets need (r, chunk)
 };
 
+__device__ __forceinline__ int sig32(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+// dQ of the wrapped slices of query block qb (slices 2qb, 2qb + 1) of slab b whose two
+// chain tails both stored their totals (fin == 2, bwd_fused): dQ = (A + B)·τ, the same
+// single add — so the same bits — as chain B's tail makes when A is done first.  The
+// totals are in bwd_fused's running-sum layout: per slice NTQ tiles of 32 x 32 fp32,
+// lane l's 16-B pieces c4 at l·16 + c4·1024, element 4 c4 + e = dQᵀ row (feature)
+// 32 cb + acc_row(4 c4 + e, l >> 5), column (query) 32 u + sig32(l & 31), tile = u·D/32 + cb.
+template <class T, int D>
+__device__ void fused_combine(const BwdParams& p, int b, int qb) {
+    constexpr int NTQ = D / 16;
+    const int NS = p.nqt, N = p.N;
+    const float* const partb = p.part + (int64_t)b * 2 * NS * NTQ * 1024;
+    const int64_t pchain = (int64_t)NS * NTQ * 1024;
+    T* const dQb = (T*)p.dQ + (int64_t)b * N * D;
+    for (int t = 2 * qb; t < 2 * qb + 2 && t < NS; ++t) {
+        if (ld_agent((gu32*)(uintptr_t)(p.fin + (int64_t)b * NS + t)) != 2u) continue;
+        for (int idx = threadIdx.x; idx < NTQ * 64; idx += 256) {
+            const int w = idx >> 6, l = idx & 63;
+            const int cb = w % (D / 32), u = w / (D / 32);
+            const int q = t * 64 + 32 * u + sig32(l & 31);
+            const float* a = partb + (int64_t)(t * NTQ + w) * 1024 + l * 4;
+            const float* bb = a + pchain;
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const f32x4 va = *(const f32x4*)(a + c4 * 256), vb = *(const f32x4*)(bb + c4 * 256);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int x = 4 * c4 + e;
+                    const int f = cb * 32 + acc_row(x, l >> 5);
+                    if (q < N) dQb[(int64_t)f * N + q] = (T)((va[e] + vb[e]) * p.scale);
+                }
+            }
+        }
+    }
+}
+
 template <class T, int D, int DV>
 __global__ __launch_bounds__(256, 2) void bwd_dq_fast(BwdParams p) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
     constexpr int KB = D * 128, VB = DV * 128, STAGE = KB + VB;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-    // fallback after bwd_fused: recompute dQ only on the slabs whose hand-off gave up
-    if (p.guard && ld_agent((gu32*)(uintptr_t)p.guard) == 0u) return;
+    // after bwd_fused: recompute dQ only on the slabs whose hand-off gave up, and make
+    // dQ = A + B of the wrapped slices whose two chain tails both stored their totals
+    const bool give_up = p.guard && ld_agent((gu32*)(uintptr_t)p.guard) != 0u;
+    const bool combine = p.cguard && ld_agent((gu32*)(uintptr_t)p.cguard) != 0u;
+    if (p.guard && !give_up && !combine) return;
     const int lid = xcd_remap(blockIdx.x, p.total_wg);
     const int b = lid / p.nblk, qb = lid - b * p.nblk;
-    if (p.sguard && ld_agent((gu32*)(uintptr_t)(p.sguard + b)) == 0u) return;
+    if (p.sguard && (!give_up || ld_agent((gu32*)(uintptr_t)(p.sguard + b)) == 0u)) {
+        if (combine) fused_combine<T, D>(p, b, qb);
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int N = p.N, Nk = p.Nk;
     const auto qrs = bslab<T>(p.Q, (int64_t)b * N * D, (int64_t)N * D);
@@ -841,12 +911,20 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // layout) and the workgroup sweeps the slab's 64-query slices.  Per slice, dS goes
 // through LDS once as a [key][query] image, and wave w computes one 32 x 32 tile of
 // dQᵀ over all 256 keys from it and the K image.  The slab's K workgroups sum each
-// slice's dQ in a FIXED order (deterministic, no atomics): member j sweeps the
+// slice's dQ in a FIXED order (deterministic, no float atomics): member j sweeps the
 // slices rotated by 3j (step i: slice (i − 3j) mod T), so the member that adds to a
-// slice after member j does so three steps later; the running fp32 sum is handed over
-// through the workspace with sc1 stores, a per-slice counter (one lane, sc1) that the
-// next member polls (one lane) before a barrier, and sc1 loads
+// slice after member j does so three steps later.  Where that order wraps from member
+// K−1 to member 0 it is cut: a slice's members form chain A (the ones that reach it
+// first, w0 .. K−1) and chain B (0 .. w0−1), each summed upwards, and dQ = A + B — one
+// add, commutative, so the same bits whoever makes it.  Every member therefore waits
+// only on the member before it, j − 1, dispatched before it.  The running fp32 sum is
+// handed over through the workspace with sc1 stores, a per-slice counter (one lane,
+// sc1) that the next member polls (one lane) before a barrier, and sc1 loads
 // (MI355X_MICROARCH § visibility, first row of the sc1 hand-off table; 1 WG per CU).
+// Chain A's tail stores its total; chain B's tail adds it in when A has finished by
+// then (always, solo: A runs ≥ 3 steps earlier) and writes dQ, else stores its own
+// total, and the second of the two tails to count in (an agent-scope atomic on the
+// slice's fin word) leaves the add to bwd_dq_fast, which runs after every single pass.
 // Step i of a member, in issue order: B1 (vmcnt(4): slice i's Q/dO DMA landed, step
 // i-1's four sum stores may still fly) | phase A, u = 0 | vmcnt(0): step i-1's sums
 // stored | u = 1 | lane 0 polls the count of step i+1's slice; the sum loads of step i
@@ -854,17 +932,15 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // i+1 | the dQ tile (asm LDS reads) | vmcnt(NDMA): the sums landed, added | the sum
 // stores (or the tail's dQ stores).  So no barrier waits on a store, and the only
 // vmcnt(0) of a step is the one in the middle of phase A.
-// Every member of a slab must be resident at once: dispatch order within an XCD
-// is monotone, so a slab's members are dealt either to one XCD (K <= 32) or across
-// all of them.  A poll gives up when its slab is missing members while the launch
-// dispatches no workgroup for 50 us (a co-tenant holds the CUs: see wait_count), or
-// after 20 ms; it then
-// sets the slab's trip word and the call's status word `err`; the slab's other polls
-// stop at once, and the guarded bwd_dq_fast that follows recomputes dQ of the slabs
-// that tripped (dK, dV do not depend on the hand-off).
+// No member needs another to be resident: dispatch within an XCD is in launch order,
+// so the lowest unfinished workgroup is always on a CU or next in line, and it waits on
+// nothing unfinished.  A co-tenant (another stream or process) can slow the chains but
+// not strand them.  A poll gives up only if the whole launch publishes nothing for
+// 100 ms (see wait_count); it then sets the slab's trip word and the call's status
+// word `err`, the slab's other polls stop at once, and the guarded bwd_dq_fast that
+// follows recomputes dQ of the slabs that tripped (dK, dV do not depend on the
+// hand-off).
 // --------------------------------------------------------------------------
-__device__ __forceinline__ int sig32(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
-
 // 16-B swizzle of the dSᵀ image, which is written by ds_write_b128 (8 groups of 8
 // contiguous lanes, banks mod 128 B) at rows sig32(r) and read only transposed.  A
 // write group covers rows {0..3} + {0, 8} (+ 4, 16, 20): the swizzle is a bijection of
@@ -890,42 +966,32 @@ __device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img,
     }
 }
 
-constexpr uint64_t kSpinTicks = 2000000;   // s_memrealtime (100 MHz): 20 ms, the bound of a poll
-
 __device__ __forceinline__ void arrive(gu32* p) {
     __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One lane waits until *f >= want, or gives up: then the slab's trip word *serr and
-// the call's status word *herr are set, and the slab's other polls stop.  Residency
-// check: every member adds 1 to its slab's arrival count *arr and to the launch's
-// *garr when it starts.  While a member of the slab is missing, the chain may wait on
-// a workgroup that cannot be dispatched until resident ones finish.  If this launch
-// still dispatches workgroups somewhere (*garr grows), the missing member is queued
-// behind this launch's own running slabs, which always progress (in-order dispatch:
-// a partial slab is at the dispatch frontier; the lowest frontier's slabs are
-// complete), so the poll keeps waiting.  A window of stall_ticks (50 us) with the slab
-// incomplete and no workgroup of the launch arriving anywhere means every resident
-// workgroup waits on CUs another process or stream holds: the poll trips.  A complete
-// slab always progresses, so for it only the 20-ms bound remains.
-__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* arr,
-                                           gu32* garr, unsigned members, uint64_t stall_ticks) {
+// One lane waits until *f >= want (its predecessor in a chain has published).  Every
+// such wait is on the previous member of the slab, of lower launch id, so it cannot
+// strand (see bwd_fused).  The poll gives up — the slab's trip word *serr and the
+// call's status word *herr are set, the slab's other polls stop — only when the
+// launch's progress count *garr (bumped by every arrival and every publish) has not
+// moved for stall_ticks (100 ms): a safety net for a dispatcher that broke launch
+// order, not a scheduling decision.  A co-tenant that holds CUs for longer than that
+// costs a recompute of the slab's dQ, never a wrong result.
+__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* garr,
+                                           uint64_t stall_ticks) {
     if (ld_agent(f) >= want) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t tw = t0;
+    uint64_t tw = __builtin_amdgcn_s_memrealtime();
     unsigned seen = ld_agent(garr);
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         if (ld_agent(f) >= want || ld_agent(serr) != 0u) return;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        bool trip = now - t0 > kSpinTicks;
-        if (now - tw > stall_ticks) {   // one window over: slab incomplete, launch not dispatching?
-            const unsigned ga = ld_agent(garr);
-            trip = trip || (ld_agent(arr) < members && ga == seen);
+        const unsigned ga = ld_agent(garr);
+        if (ga != seen) {
             seen = ga;
             tw = now;
-        }
-        if (trip) {
+        } else if (now - tw > stall_ticks) {
             st_agent(serr, 1u);
             st_agent(herr, 1u);
             return;
@@ -980,12 +1046,14 @@ __device__ __forceinline__ u32x4 desc_of(const void* base, uint32_t bytes) {
 // Vector-memory operations hidden from the compiler's waitcnt model: the caller
 // counts vmcnt for them (they retire in issue order) and fences the results.
 __device__ __forceinline__ void dma16_asm(const u32x4& desc, uint32_t lds_base, int voff) {
-    asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
+    // s_nop 4: five wait states between a VALU write of the descriptor SGPRs (v_readlane
+    // of a spilled SGPR, which the hazard recognizer cannot see past the asm) and the read
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
 }
 template <int OFF>
 __device__ __forceinline__ u32x4 load16_sc1_asm(const u32x4& desc, int voff) {
     u32x4 r;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 sc1" : "=v"(r) : "v"(voff), "s"(desc), "i"(OFF) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 sc1" : "=v"(r) : "v"(voff), "s"(desc), "i"(OFF) : "memory");
     return r;
 }
 // dma_image8 through dma16_asm; returns nothing, issues (R/8 + 7)/8 ops or fewer per wave
@@ -1051,7 +1119,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const float c = p.scale_log2;
     const float* nlse = p.nlse + (int64_t)b * N;
     const float* nDg = p.nD + (int64_t)b * N;
-    const int64_t pslab = (int64_t)NS * NTQ * 1024;   // floats of running sums per slab
+    const int64_t pslab = (int64_t)2 * NS * NTQ * 1024;   // floats of running sums per slab (two chains)
+    const int pchain4 = NS * NTQ * 4096;                  // bytes of one chain's sums
     const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.part + b * pslab), (short)0, (int)(pslab * 4),
                                                        0x00020000);
     const u32x4 pdesc = desc_of(p.part + b * pslab, (uint32_t)(pslab * 4));
@@ -1059,20 +1128,19 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const u32x4 odesc = desc_of((const T*)p.dO + (int64_t)b * N * DV, (uint32_t)(N * DV * 2));
     // this wave's loop DMA ops per slice (dma_image8_asm), >= for every wave: a lower bound
     constexpr int NDMA = (D / 8 >= 8 ? D / 64 : 0) + (DV / 8 >= 8 ? DV / 64 : 0);
-    gu32* const flg = (gu32*)(p.flags + (int64_t)b * NS);
+    const FusedFlags ff = fused_flags(p.batch, NS, KM);
+    gu32* const cnt0 = (gu32*)(p.flags + ff.cnt + (int64_t)b * NS);               // chain A's per-slice counts
+    gu32* const cnt1 = (gu32*)(p.flags + ff.cnt + (int64_t)(p.batch + b) * NS);   // chain B's
+    gu32* const fin = (gu32*)(p.flags + ff.fin + (int64_t)b * NS);                // tails that stored (wrapped slices)
     gu32* const err = (gu32*)p.err;
-    gu32* const arr = (gu32*)(p.flags + (int64_t)p.batch * NS + b);               // this slab's arrival count
-    gu32* const serr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 1) + b);        // and its trip word
-    gu32* const xmask = (gu32*)(p.flags + (int64_t)p.batch * (NS + 2) + b);       // the XCDs of its members
-    gu32* const garr = (gu32*)(p.flags + (int64_t)p.batch * (NS + 3));            // the launch's arrival count
+    gu32* const serr = (gu32*)(p.flags + ff.serr + b);                            // this slab's trip word
+    gu32* const xccw = (gu32*)(p.flags + ff.xcc + (int64_t)b * KM);               // its members' XCDs + 1
+    gu32* const garr = (gu32*)(p.flags + ff.garr);                                // the launch's progress count
+    gu32* const comb = (gu32*)(p.flags + ff.comb);
     const uint64_t stall = (uint64_t)p.stall_ticks;
+    const unsigned my_xcc = (__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u) + 1u;   // HW_REG_XCC_ID[3:0]
     if (tid == 0) {
-        if (p.l2local) {   // this member's XCD into the slab's mask, acknowledged before it counts as arrived
-            const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID[3:0]
-            __hip_atomic_fetch_or(xmask, 1u << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        arrive(arr);
+        st_agent(xccw + j, my_xcc);
         arrive(garr);
     }
 
@@ -1100,13 +1168,33 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         int t = (i - OFF * j) % NS;
         return t < 0 ? t + NS : t;
     };
-    // chain position of this member for slice t: the members that reach t first
-    // (steps (t + OFF·j') mod NS ascending) are j' >= ceil((NS − t)/OFF), then 0, 1, ...
-    auto chain_pos = [&](int t) {
+    // this member's link in slice t's chains: the members that reach t first (steps
+    // (t + OFF·j') mod NS ascending) are j' >= w0 = ceil((NS − t)/OFF); when w0 < KM the
+    // order wraps and is cut there into chain A = w0 .. KM−1 (ch 0) and B = 0 .. w0−1
+    // (ch 1), else one chain 0 .. KM−1
+    struct Link {
+        int ch, pos, len;
+        bool wrap;
+    };
+    auto link_of = [&](int t) {
         const int w0 = (NS - t + OFF - 1) / OFF;
-        const int head = w0 < KM ? w0 : 0;
-        const int pos = j - head;
-        return pos < 0 ? pos + KM : pos;
+        Link L;
+        L.wrap = w0 < KM;
+        L.ch = L.wrap && j < w0 ? 1 : 0;
+        L.pos = L.wrap && j >= w0 ? j - w0 : j;
+        L.len = !L.wrap ? KM : L.ch ? w0 : KM - w0;
+        return L;
+    };
+    // a publish after the step's sums left: the chain's count, or for the tail of a
+    // wrapped slice's chain the slice's fin word (the second tail leaves A + B to
+    // bwd_dq_fast); every publish counts as progress of the launch
+    auto publish = [&](int tp, int posp, int chp, int kind) {
+        if (kind == 1) {
+            st_agent((chp ? cnt1 : cnt0) + tp, (unsigned)(posp + 1));
+        } else if (__hip_atomic_fetch_add(fin + tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+            st_agent(comb, 1u);
+        }
+        arrive(garr);
     };
     auto load_rowc = [&](int t) {
         const int q = t * 64 + (tid & 63);
@@ -1148,33 +1236,32 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const int dsrow = 32 * wave + sig32(r);                  // this lane's dSᵀ row
     const int cbq = wave % (D / 32), uq = wave / (D / 32);   // this wave's dQᵀ tile (wave < NTQ)
 
-    // L2-local hand-off: when every member of the slab runs on one XCD (the xcd mapping
-    // deals them so; the mask checks it), the running sums are stored plainly and stay in
-    // that XCD's L2, where the next member's sc1 loads (L1 bypass, L2-served) find them;
-    // otherwise sc1 stores (L2 write-through, dropped) as everywhere else.  Decided once
-    // every member has arrived (a stalled arrival trips the slab as in wait_count).
+    // the prologue's loads have landed: no LDS-DMA the compiler knows of is pending in
+    // the loop (its DMA is asm), so it adds no vmcnt(0) before the loop's LDS reads
+    vm_wait<0>();
+    // L2-local hand-off: when the next member (j + 1, the reader of every running sum this
+    // one hands on) has already arrived on this member's XCD, the sums are stored plainly
+    // and stay in that XCD's L2, where its sc1 loads (L1 bypass, L2-served) find them;
+    // otherwise — or not there yet: nothing waits for it — sc1 stores (L2 write-through,
+    // dropped) as everywhere else.  A chain's tail stores sc1 always.
     __shared__ unsigned s_local;
+    __shared__ unsigned s_direct[2];   // chain B's tail of step i's slice: A had finished (slot i & 1)
     bool local = false;
     if (p.l2local) {
-        if (tid == 0) {
-            wait_count(arr, (unsigned)KM, serr, err, arr, garr, (unsigned)KM, stall);
-            const unsigned m = ld_agent(xmask);
-            s_local = (ld_agent(arr) >= (unsigned)KM && (m & (m - 1u)) == 0u) ? 1u : 0u;
-        }
+        if (tid == 0) s_local = (j + 1 < KM && ld_agent(xccw + j + 1) == my_xcc) ? 1u : 0u;
         __syncthreads();
         local = s_local != 0u;
     }
 
-    int t_prev = 0, pos_prev = 0;
-    bool pub_prev = false;
-    // the prologue's loads have landed: no LDS-DMA the compiler knows of is pending in
-    // the loop (its DMA is asm), so it adds no vmcnt(0) before the loop's LDS reads
-    vm_wait<0>();
+    int t_prev = 0, pos_prev = 0, ch_prev = 0, pub_prev = 0;   // pub_prev: 0 none, 1 chain count, 2 fin word
     for (int i = 0; i < NS; ++i) {
         t = slice_of(i);
-        const int pos = chain_pos(t);
+        const Link lk = link_of(t);
+        const int pos = lk.pos;
+        gu32* const cnt = lk.ch ? cnt1 : cnt0;
         const int tq = opaque(tid), lq = tq & 63, rq = lq & 31, hq = lq >> 5;   // re-derived per step
-        const bool tail = pos == KM - 1;
+        const bool tail = pos == lk.len - 1;
+        const bool btail = lk.wrap && tail && lk.ch == 1;   // chain B's tail: makes A + B when A is done
         // B1: this slice's images landed; lane 0 has seen the predecessor's count for
         // slice t (polled at the end of the previous step's dQ phase, or here for the
         // first step; the barrier releases the other waves' sum loads).  The previous
@@ -1185,11 +1272,14 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         const bool has_tile = NTQ >= 8 || wave < NTQ;
         if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
-        if (i == 0 && pos > 0 && tid == 0 && !(abl & 1)) wait_count(flg + t, (unsigned)pos, serr, err, arr, garr, (unsigned)KM, stall);
+        if (i == 0 && tid == 0 && !(abl & 1)) {
+            if (pos > 0) wait_count(cnt + t, (unsigned)pos, serr, err, garr, stall);
+            if (btail) s_direct[0] = ld_agent(fin + t) >= 1u ? 1u : 0u;
+        }
         __syncthreads();
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
-        const int pofs = (t * NTQ + wave) * 4096 + lq * 16;
+        const int pofs = lk.ch * pchain4 + (t * NTQ + wave) * 4096 + lq * 16;
         const bool ldpin = pos > 0 && has_tile && !(abl & 10);
         u32x4 pin[4];
 #pragma unroll
@@ -1238,8 +1328,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // (drained in the middle of this phase), so the poll pays only its own latency,
         // and barriers B2 and B1 order it before every wave's sum loads of that step
         if (wave == 0 && i + 1 < NS && !(abl & 1)) {
-            const int tn = slice_of(i + 1), pn = chain_pos(tn);
-            if (pn > 0 && tq == 0) wait_count(flg + tn, (unsigned)pn, serr, err, arr, garr, (unsigned)KM, stall);
+            const int tn = slice_of(i + 1);
+            const Link ln = link_of(tn);
+            if (tq == 0) {
+                if (ln.pos > 0) wait_count((ln.ch ? cnt1 : cnt0) + tn, (unsigned)ln.pos, serr, err, garr, stall);
+                if (ln.wrap && ln.ch == 1 && ln.pos == ln.len - 1)
+                    s_direct[(i + 1) & 1] = ld_agent(fin + tn) >= 1u ? 1u : 0u;
+            }
         }
         if (has_tile && !(abl & 10)) {
             pin[0] = load16_sc1_asm<0>(pdesc, pofs);
@@ -1248,7 +1343,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             pin[3] = load16_sc1_asm<3072>(pdesc, pofs);
         }
         __syncthreads();   // B2: dSᵀ complete, the slice's images free, last step's sums stored
-        if (pub_prev && tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
+        // chain B's tail: whether A's total was there at the poll (lane 0's word, ordered
+        // by B2).  Read and waited for here: the dQ phase below counts its own LDS reads
+        // by hand (lgkm_wait), so no compiler-issued LDS read may land among them.
+        const unsigned dword = btail ? s_direct[i & 1] : 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const bool direct = btail && __builtin_amdgcn_readfirstlane(dword) != 0u;
+        if (pub_prev && tid == 0) publish(t_prev, pos_prev, ch_prev, pub_prev);
 
         // next slice's images and row constants (land before the next B1)
         // (the last step reloads its own slice: harmless, nothing reads it)
@@ -1319,7 +1420,23 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pin[c4][e]);
             }
-            if (tail) {
+            // chain B's tail with A finished: A's total (its tail's sc1 stores, published
+            // through fin before this step's poll) in, after this chain's own sum
+            if (direct) {
+                const int pofa = pofs - pchain4;
+                pin[0] = load16_sc1_asm<0>(pdesc, pofa);
+                pin[1] = load16_sc1_asm<1024>(pdesc, pofa);
+                pin[2] = load16_sc1_asm<2048>(pdesc, pofa);
+                pin[3] = load16_sc1_asm<3072>(pdesc, pofa);
+                vm_wait<0>();
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    reg_fence(pin[c4]);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pin[c4][e]);
+                }
+            }
+            if ((tail && !lk.wrap) || direct) {
                 // 32-bit lane offset + scalar row offset (no hoisted 64-bit addresses)
                 const int q = t * 64 + 32 * uq + sig32(rq);
                 const auto qo = bslab<T>(p.dQ, (int64_t)b * N * D, (int64_t)N * D);
@@ -1333,19 +1450,20 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 for (int c4 = 0; c4 < 4; ++c4) {
                     const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
                                       __float_as_uint(acc[4 * c4 + 2]), __float_as_uint(acc[4 * c4 + 3])};
-                    if (local) __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 0);
+                    if (local && !tail) __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 0);
                     else __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);   // sc1
                 }
             }
         }
         t_prev = t;
         pos_prev = pos;
-        pub_prev = !tail;
+        ch_prev = lk.ch;
+        pub_prev = (tail && !lk.wrap) || direct ? 0 : tail ? 2 : 1;
     }
     if (pub_prev) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) st_agent(flg + t_prev, (unsigned)(pos_prev + 1));
+        if (tid == 0) publish(t_prev, pos_prev, ch_prev, pub_prev);
     }
     if (key_ok) {
         const auto ko = bslab<T>(p.dK, (int64_t)b * Nk * D, (int64_t)Nk * D);
@@ -1381,7 +1499,7 @@ thread_local int g_bwd_mode = env_bwd_mode();   // 0 auto, 1 split passes, 2 sin
 thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD
                                             // (-1 auto: at d, dv <= 64; 0 never; 1 always)
 thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members
-thread_local int g_bwd_stall_us = kStallUs; // bwd_fused: residency-check window
+thread_local int g_bwd_stall_us = kStallUs; // bwd_fused: no-progress bound of a poll (us)
 thread_local int g_bwd_xcd = -1;            // bwd_fused: one XCD per slab where eligible (-1 auto, 0 never)
 
 template <class T, int D, int DV>
@@ -1390,8 +1508,11 @@ static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
     if (fused) {   // single pass; dQ pass below only after a hand-off timeout
         p.total_wg = p.nkb * p.batch;
         hipLaunchKernelGGL((bwd_fused<T, D, DV>), dim3((unsigned)p.total_wg), dim3(512), 0, s, p);
+        const FusedFlags ff = fused_flags(p.batch, p.nqt, p.nkb);
         p.guard = p.err;
-        p.sguard = p.flags + (int64_t)p.batch * (p.nqt + 1);
+        p.sguard = p.flags + ff.serr;
+        p.cguard = p.flags + ff.comb;
+        p.fin = p.flags + ff.fin;
     }
     p.nblk = (p.N + 127) / 128;
     p.total_wg = p.nblk * p.batch;
@@ -1466,10 +1587,10 @@ static BwdPad pad_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, 
 
 // Single-pass plan (bwd_fused) on the shape the fast kernels run (padded or not):
 // K = ceil(Nk/256) members per slab, T = ceil(N/64) slices, step offset 3 (needs
-// 3K <= T); every member of a slab resident at once (K <= CUs; one XCD per slab
-// when K <= CUs/8 and the slab count is a multiple of 8); auto only when the grid
-// fills the chip once.  Workspace: per-slice counters, per-slab arrival counts, trip words and XCD masks, then the
-// running fp32 dQ sums (4·N·d bytes per slab).
+// 3K <= T); K <= CUs, one XCD per slab when K <= CUs/8 and the slab count is a
+// multiple of 8 (a slab's members then run together: speed, not correctness, which
+// needs no co-residency); auto only when the grid fills the chip once.  Workspace: the hand-off words (FusedFlags), then the two chains'
+// running fp32 dQ sums (2 x 4·N·d bytes per slab).
 struct FusedPlan {
     bool on = false;
     int nkb = 0, nqt = 0, xcd = 0;
@@ -1481,7 +1602,7 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
     const int cus = device_cus(s);
-    if (cus < 8 || g_bwd_hoff * K > T || K > cus || batch * K > INT32_MAX / 2 || T * (d / 16) * 4096 >= INT32_MAX) return f;
+    if (cus < 8 || g_bwd_hoff * K > T || K > cus || batch * K > INT32_MAX / 2 || 2 * T * (d / 16) * 4096 >= INT32_MAX) return f;
     const int xcd = (K <= cus / 8 && batch % 8 == 0 && g_bwd_xcd != 0) ? 1 : 0;
     if (g_bwd_mode == 0) {
         // auto: the grid fills the chip, and K divides the CUs a slab's members are dealt
@@ -1492,9 +1613,8 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     f.nkb = (int)K;
     f.nqt = (int)T;
     f.xcd = xcd;
-    f.flag_bytes = al256((size_t)(batch * T + 3 * batch + 1) * 4);   // slice counters; slab arrivals, trip words,
-                                                                    // XCD masks; the launch's arrival count
-    f.bytes = f.flag_bytes + al256((size_t)(batch * T * (d / 16)) * 4096) + 256;
+    f.flag_bytes = al256((size_t)fused_flags(batch, T, K).words * 4);   // FusedFlags
+    f.bytes = f.flag_bytes + al256((size_t)(2 * batch * T * (d / 16)) * 4096) + 256;   // two chains' running sums
     return f;
 }
 
@@ -1617,7 +1737,7 @@ static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStr
 #endif
     hipError_t e = hipMemsetAsync(w, 0, fz.flag_bytes, s);
     if (e == hipSuccess && g_bwd_mode == 3)
-        e = hipMemsetD32Async((hipDeviceptr_t)(p.flags + (int64_t)p.batch * (fz.nqt + 1)), 1u, (size_t)p.batch, s);
+        e = hipMemsetD32Async((hipDeviceptr_t)(p.flags + fused_flags(p.batch, fz.nqt, fz.nkb).serr), 1u, (size_t)p.batch, s);
     return e;
 }
 

@@ -336,12 +336,14 @@ def test_backward_handoff_status_errors(fa):
 
 def test_backward_two_streams_concurrent(fa):
     """Two configs[3]-sized backward calls (N 8192, d 128, 64 slabs) on two streams at
-    once: each single pass needs all 32 members of a slab resident, and the other
-    stream holds CUs, so slabs of the two calls can wait on each other's CUs.  The
-    residency check (fa_bwd.hip wait_count) must trip such a slab within tens of us and
-    recompute only its dQ: the pair's wall time stays within 1.6x the same two calls
-    run back to back on one stream (a 20-ms poll bound would cost ~7x), and both
-    results match the float64 oracle on one slab each."""
+    once, each holding CUs the other's single pass would use.  Every hand-off wait of
+    the single pass is on a member of lower launch id (two chains per slice, cut where
+    the rotated order wraps: fa_bwd.hip bwd_fused), so neither call can strand: both
+    must complete their hand-off (status 0 on every concurrent call, no slab given up
+    and recomputed) and match the float64 oracle on one slab each.  Timing is reported,
+    and bounded only loosely (2.5x the same pair back to back on one stream, against
+    ~7x for round 3's stalled chains): the mechanism is what the test asserts, not a
+    ratio within the 5-7 % box-to-box variance."""
     import time
     N, d, BH = 8192, 128, 64
     g = torch.Generator(device="cuda").manual_seed(23)
@@ -370,14 +372,16 @@ def test_backward_two_streams_concurrent(fa):
         return outs, status, dt
 
     pair(False); pair(True)   # warm up (allocations, code objects, clocks)
-    serial = min(pair(False)[2] for _ in range(3))
-    runs = [pair(True) for _ in range(3)]
-    outs, status, _ = runs[-1]
-    conc = min(r[2] for r in runs)
-    print(f"two-stream backward: serial pair {serial * 1e3:.2f} ms, concurrent pair "
-          f"{[round(r[2] * 1e3, 2) for r in runs]} ms, hand-off status {[r[1] for r in runs]}")
-    assert all(s in (-1, 0, 1) for r in runs for s in r[1])
-    assert conc <= 1.6 * serial, f"concurrent pair {conc * 1e3:.2f} ms vs serial {serial * 1e3:.2f} ms"
+    runs = []
+    for _ in range(3):   # interleaved repetitions
+        runs.append((pair(False), pair(True)))
+    serial = sorted(r[0][2] for r in runs)[1]
+    conc = sorted(r[1][2] for r in runs)[1]
+    print(f"two-stream backward: serial pair {[round(r[0][2] * 1e3, 2) for r in runs]} ms, concurrent pair "
+          f"{[round(r[1][2] * 1e3, 2) for r in runs]} ms, hand-off status {[r[1][1] for r in runs]}")
+    assert all(r[0][1] == [0] and r[1][1] == [0, 0] for r in runs), [(r[0][1], r[1][1]) for r in runs]
+    assert conc <= 2.5 * serial, f"concurrent pair {conc * 1e3:.2f} ms vs serial {serial * 1e3:.2f} ms (medians)"
+    outs = runs[-1][1][0]
     for i, b in ((0, 5), (1, 40)):
         Q, K, V, Oo, dO, l, m = ins[i]
         sl = lambda t: _np(t[:, :, b:b + 1])
@@ -385,6 +389,37 @@ def test_backward_two_streams_concurrent(fa):
                                             _np(l[:, :, b:b + 1]), _np(m[:, :, b:b + 1]))
         for a, r_, nm in zip(outs[i], (dqr, dkr, dvr), ("dQ", "dK", "dV")):
             assert_grad_close(sl(a), r_, "bfloat16", f"stream {i} {nm}")
+
+
+@pytest.mark.parametrize("N,Nk,d,BH,xcd", [(16384, 16384, 128, 64, -1), (8192, 6144, 128, 96, 0),
+                                          (4096, 3072, 64, 200, -1)])
+def test_backward_single_pass_multipass_grid_solo(fa, N, Nk, d, BH, xcd):
+    """Solo calls whose single-pass grid takes several passes over the chip (64 members x
+    64 slabs = 16 passes; 24 members — not a divisor of the CUs — dealt chip-wide, forced;
+    12 members x 200 slabs) complete the hand-off (status 0: no slab gives up while the
+    launch still dispatches), and dQ is bitwise reproducible."""
+    L = fa.lib()
+    g = torch.Generator(device="cuda").manual_seed(N + Nk + BH)
+    mk = lambda n: fa.jl_tensor(torch.randn((n, d, BH), generator=g, device="cuda"), torch.bfloat16)
+    Q, K, V, dO = mk(N), mk(Nk), mk(Nk), mk(N)
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    old_x = L.fa_debug_set_bwd_xcd(xcd)
+    try:
+        st = []
+        one = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m, status=st)
+        one = [t.clone() for t in one]
+        again = _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m, status=st)
+    finally:
+        L.fa_debug_set_bwd_xcd(old_x)
+    assert st == [0, 0], st
+    for a, b_, nm in zip(one, again, ("dQ", "dK", "dV")):
+        assert torch.equal(a, b_), nm + " not reproducible"
+    b = BH - 1
+    sl = lambda t: _np(t[:, :, b:b + 1])
+    dqr, dkr, dvr = O.dense_fa_backward(sl(Q), sl(K), sl(V), sl(Oo), sl(dO), _np(l[:, :, b:b + 1]),
+                                        _np(m[:, :, b:b + 1]))
+    for a, r_, nm in zip(one, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+        assert_grad_close(sl(a), r_, "bfloat16", nm)
 
 
 _SPLIT_CHILD = r"""
