@@ -293,7 +293,7 @@ def _mfma_roofline(flops, seconds, kernel, note=None):
     return r
 
 
-def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5, split=False):
+def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
     """BASELINE configs[3]: dense_fa bf16 (B,H,N,d) = (4,16,8192,128) forward,
     backward (reference src/dense.jl:104-167, executable spec
     src_cpp/FlashAttention.cpp:194-252) and forward+backward.  FLOPs: forward
@@ -309,15 +309,14 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5, split=False):
     _, e_f = time_region(lambda: fa.dense_fa_(O, l, m, Q, K, V), steps_fwd, 2, dist)
     t_f = e_f / steps_fwd
     k_f = _fwd_kernel_128(fa)
+    fa.dense_fa_backward(Q, K, V, O, dO, l, m)   # the stream's scratch buffer exists before the count is read
+    trips0 = fa.backward_handoff_trips(Q.device)
     _, e_b = time_region(lambda: fa.dense_fa_backward(Q, K, V, O, dO, l, m), steps_bwd, 1, dist)
     t_b = e_b / steps_bwd
     hs = fa.backward_handoff_status(Q.device)   # the last timed call
-    # each call's pre-pass rewrites the status word, so the earlier timed calls are
-    # re-checked one by one in an untimed pass: any timeout marks the block tainted
-    hs_calls = []
-    for _ in range(steps_bwd):
-        fa.dense_fa_backward(Q, K, V, O, dO, l, m)
-        hs_calls.append(fa.backward_handoff_status(Q.device))
+    # slabs that gave up over the warm-up and timed calls: a counter in the workspace
+    # header that no call resets (fa_hip.backward_handoff_trips), read around them
+    trips = (fa.backward_handoff_trips(Q.device) - trips0) & 0xFFFFFFFF
     res = {
         "workload": "configs[3]: dense_fa bf16 forward + backward, (B,H,N,d)=(4,16,8192,128)",
         "fwd_tflops": f / t_f / 1e12, "bwd_tflops": 2.5 * f / t_b / 1e12,
@@ -325,15 +324,14 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5, split=False):
         "fwd_ms": t_f * 1e3, "bwd_ms": t_b * 1e3, "steps_fwd": steps_fwd, "steps_bwd": steps_bwd,
         "roofline_fwd": _mfma_roofline(f, t_f, k_f),
         "roofline_bwd": _mfma_roofline(
-            2.5 * f, t_b, "fa::bwd_dkdv_fast + fa::bwd_dq_fast" if split else "fa::bwd_fused<bf16,128,128>",
-            "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + " +
-            ("the split dK/dV and dQ passes), " if split else "bwd_fused + the guarded dQ pass), ") +
+            2.5 * f, t_b, "fa::bwd_fused<bf16,128,128>",
+            "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + bwd_fused + the guarded dQ pass), "
             "FLOPs = 2.5x forward (the 5 GEMMs of the single pass)"),
         "roofline_fwd_bwd": _mfma_roofline(3.5 * f, t_f + t_b, "forward + backward calls"),
         "bwd_handoff": {-1: "two-pass plan (no hand-off)", 0: "single pass, hand-off completed",
                         1: "single pass, a slab's hand-off GAVE UP (members not co-resident): its dQ recomputed by the guarded pass"}.get(hs, hs),
-        "bwd_handoff_recheck": hs_calls,
-        "bwd_fallback_tainted": any(x == 1 for x in hs_calls + [hs]),
+        "bwd_handoff_giveups": trips,
+        "bwd_fallback_tainted": trips != 0 or hs == 1,
     }
     del Q, K, V, dO, O, l, m
     torch.cuda.empty_cache()
@@ -590,13 +588,6 @@ def main():
         step = _cpu_hook_step(rank)
         sync, events = (lambda: None), False
     else:
-        if shared_gpu:
-            # co-tenant ranks: the single-pass backward needs every member of a slab
-            # resident at once, which another process's kernels on the same CUs defeat
-            # (it trips and recomputes dQ: 16-18 ms per configs[3] call against 14.1 for
-            # the split passes, profiles/r04_bwd_two_process_placement.log); the
-            # deployment switch, read when the library loads
-            os.environ["FA_HIP_BWD_SPLIT"] = "1"
         import fa_hip
         fa_hip.lib()
         BH = B_ * H_
@@ -650,9 +641,11 @@ def main():
         out["cpu_step_hook"] = True
 
     if not args.no_cfg23 and not cpu_hook:
-        out["cfg3"] = cfg3_block(fa_hip, dist, split=shared_gpu)
+        out["cfg3"] = cfg3_block(fa_hip, dist)
         if shared_gpu:
-            out["cfg3"]["bwd_plan"] = "split passes: the ranks share one GPU"
+            # co-tenant ranks: the single pass needs no co-residency (every hand-off wait
+            # is on an earlier-dispatched workgroup), so it stays the plan here too
+            out["cfg3"]["bwd_plan"] = "single pass: the ranks share one GPU"
         out["cfg2"] = cfg2_block(fa_hip, dist)
     if not args.no_cfg4:
         out["cfg4"] = cfg4_block(fa_hip, world, rank, dist, args.cfg4_steps, 1, cpu_hook)

@@ -39,7 +39,8 @@ struct FusedFlags {
     int64_t fin;    // [batch][NS]: tails of a wrapped slice's two chains that stored their sums
     int64_t serr;   // [batch]: the slab gave up (its dQ is recomputed by bwd_dq_fast)
     int64_t xcc;    // [batch][KM]: XCD of each member + 1 (L2-local hand-off)
-    int64_t garr;   // the launch's progress count (arrivals and publishes)
+    int64_t prog;   // [batch][KM]: each member's count of publishes (plain stores, no contention)
+    int64_t garr;   // the launch's arrival count (one add per workgroup)
     int64_t comb;   // a wrapped slice is left to bwd_dq_fast's combine
     int64_t words;
 };
@@ -49,7 +50,8 @@ __host__ __device__ inline FusedFlags fused_flags(int64_t batch, int64_t NS, int
     f.fin = 2 * batch * NS;
     f.serr = 3 * batch * NS;
     f.xcc = f.serr + batch;
-    f.garr = f.xcc + batch * KM;
+    f.prog = f.xcc + batch * KM;
+    f.garr = f.prog + batch * KM;
     f.comb = f.garr + 1;
     f.words = f.comb + 1;
     return f;
@@ -69,7 +71,8 @@ struct BwdParams {
     unsigned* flags = nullptr;   // hand-off words (FusedFlags, zeroed per call)
     unsigned* err = nullptr;     // hand-off timeout word = hdr[1] (set per call by the pre-pass)
     // workspace header (first 256 B of the aligned workspace; fa_dense_bwd_handoff_status):
-    // hdr[0] = kBwdHdrMagic | plan (1 = single pass), hdr[1] = the timeout word
+    // hdr[0] = kBwdHdrMagic | plan (1 = single pass), hdr[1] = the timeout word,
+    // hdr[2] = give-ups counted over every call on this workspace (never reset here)
     unsigned* hdr = nullptr;
     unsigned hdr_plan = 0, hdr_err = 0;
     float* part = nullptr;       // [batch][2 chains][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
@@ -923,8 +926,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // (MI355X_MICROARCH § visibility, first row of the sc1 hand-off table; 1 WG per CU).
 // Chain A's tail stores its total; chain B's tail adds it in when A has finished by
 // then (always, solo: A runs ≥ 3 steps earlier) and writes dQ, else stores its own
-// total, and the second of the two tails to count in (an agent-scope atomic on the
-// slice's fin word) leaves the add to bwd_dq_fast, which runs after every single pass.
+// total and leaves the add to bwd_dq_fast, which runs after every single pass (the
+// slice's fin word, an agent-scope counter both tails add to, reads 2 then).
 // Step i of a member, in issue order: B1 (vmcnt(4): slice i's Q/dO DMA landed, step
 // i-1's four sum stores may still fly) | phase A, u = 0 | vmcnt(0): step i-1's sums
 // stored | u = 1 | lane 0 polls the count of step i+1's slice; the sum loads of step i
@@ -973,27 +976,43 @@ __device__ __forceinline__ void arrive(gu32* p) {
 // One lane waits until *f >= want (its predecessor in a chain has published).  Every
 // such wait is on the previous member of the slab, of lower launch id, so it cannot
 // strand (see bwd_fused).  The poll gives up — the slab's trip word *serr and the
-// call's status word *herr are set, the slab's other polls stop — only when the
-// launch's progress count *garr (bumped by every arrival and every publish) has not
-// moved for stall_ticks (100 ms): a safety net for a dispatcher that broke launch
-// order, not a scheduling decision.  A co-tenant that holds CUs for longer than that
-// costs a recompute of the slab's dQ, never a wrong result.
-__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* garr,
-                                           uint64_t stall_ticks) {
+// call's status word *herr are set, the slab's other polls stop — only when neither
+// the launch's arrival count *garr nor any publish count of the slab's KM members
+// (prog[], one plain store per member and step: a single launch-wide counter bumped
+// per publish measured 5 % slower, its atomics queueing on one address) has moved for
+// stall_ticks (100 ms): a safety net for a dispatcher that broke launch order, not a
+// scheduling decision.  A co-tenant that holds CUs for longer than that costs a
+// recompute of the slab's dQ, never a wrong result.
+__device__ __forceinline__ void wait_count(gu32* f, unsigned want, gu32* serr, gu32* herr, gu32* garr, gu32* prog,
+                                           int KM, uint64_t stall_ticks) {
     if (ld_agent(f) >= want) return;
-    uint64_t tw = __builtin_amdgcn_s_memrealtime();
-    unsigned seen = ld_agent(garr);
+    auto progress = [&]() {
+        unsigned sum = ld_agent(garr);
+        for (int k = 0; k < KM; ++k) sum += ld_agent(prog + k);
+        return sum;
+    };
+    // the progress counts are first read after 20 us of waiting (not at entry: a
+    // short wait — the common case — then costs no more than the polls themselves)
+    uint64_t tw = __builtin_amdgcn_s_memrealtime(), tc = tw;
+    unsigned seen = 0u;
+    bool have = false;
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         if (ld_agent(f) >= want || ld_agent(serr) != 0u) return;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        const unsigned ga = ld_agent(garr);
-        if (ga != seen) {
-            seen = ga;
+        if (now - tc < 2000) continue;   // look at the progress counts every 20 us
+        tc = now;
+        const unsigned pg = progress();
+        if (!have || pg != seen) {
+            have = true;
+            seen = pg;
             tw = now;
         } else if (now - tw > stall_ticks) {
             st_agent(serr, 1u);
             st_agent(herr, 1u);
+            // hdr[2]: a count of give-ups the pre-pass never resets (callers read it
+            // around a series of calls: fa_hip.backward_handoff_trips)
+            __hip_atomic_fetch_add(herr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
     }
@@ -1135,7 +1154,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     gu32* const err = (gu32*)p.err;
     gu32* const serr = (gu32*)(p.flags + ff.serr + b);                            // this slab's trip word
     gu32* const xccw = (gu32*)(p.flags + ff.xcc + (int64_t)b * KM);               // its members' XCDs + 1
-    gu32* const garr = (gu32*)(p.flags + ff.garr);                                // the launch's progress count
+    gu32* const garr = (gu32*)(p.flags + ff.garr);                                // the launch's arrival count
+    gu32* const prog = (gu32*)(p.flags + ff.prog + (int64_t)b * KM);              // the slab's publish counts
     gu32* const comb = (gu32*)(p.flags + ff.comb);
     const uint64_t stall = (uint64_t)p.stall_ticks;
     const unsigned my_xcc = (__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u) + 1u;   // HW_REG_XCC_ID[3:0]
@@ -1186,15 +1206,20 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         return L;
     };
     // a publish after the step's sums left: the chain's count, or for the tail of a
-    // wrapped slice's chain the slice's fin word (the second tail leaves A + B to
-    // bwd_dq_fast); every publish counts as progress of the launch
+    // wrapped slice's chain an add to the slice's fin word (no return value: a returning
+    // atomic would make this wave wait for the step's running-sum loads).  fin == 2
+    // after the launch means both tails stored their totals: chain B's tail found A
+    // unfinished, stored instead of writing dQ, and flagged the launch (comb) so that
+    // bwd_dq_fast adds them.  Every publish counts as progress of the slab (prog).
+    unsigned npub = 0;
     auto publish = [&](int tp, int posp, int chp, int kind) {
         if (kind == 1) {
             st_agent((chp ? cnt1 : cnt0) + tp, (unsigned)(posp + 1));
-        } else if (__hip_atomic_fetch_add(fin + tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
-            st_agent(comb, 1u);
+        } else {
+            __hip_atomic_fetch_add(fin + tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (chp == 1) st_agent(comb, 1u);
         }
-        arrive(garr);
+        st_agent(prog + j, (unsigned)++npub);
     };
     auto load_rowc = [&](int t) {
         const int q = t * 64 + (tid & 63);
@@ -1239,18 +1264,25 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     // the prologue's loads have landed: no LDS-DMA the compiler knows of is pending in
     // the loop (its DMA is asm), so it adds no vmcnt(0) before the loop's LDS reads
     vm_wait<0>();
-    // L2-local hand-off: when the next member (j + 1, the reader of every running sum this
-    // one hands on) has already arrived on this member's XCD, the sums are stored plainly
-    // and stay in that XCD's L2, where its sc1 loads (L1 bypass, L2-served) find them;
-    // otherwise — or not there yet: nothing waits for it — sc1 stores (L2 write-through,
-    // dropped) as everywhere else.  A chain's tail stores sc1 always.
-    __shared__ unsigned s_local;
+    // L2-local hand-off: once the next member (j + 1, the reader of every running sum
+    // this one hands on) is known to run on this member's XCD, the sums are stored
+    // plainly and stay in that XCD's L2, where its sc1 loads (L1 bypass, L2-served) find
+    // them; until then — nothing waits for it: lane 0 looks for its XCD word once per
+    // step while it is missing — sc1 stores (L2 write-through, dropped) as everywhere
+    // else.  A chain's tail stores sc1 always.
+    __shared__ unsigned s_local;       // read after B2 of each step
     __shared__ unsigned s_direct[2];   // chain B's tail of step i's slice: A had finished (slot i & 1)
-    bool local = false;
-    if (p.l2local) {
-        if (tid == 0) s_local = (j + 1 < KM && ld_agent(xccw + j + 1) == my_xcc) ? 1u : 0u;
-        __syncthreads();
-        local = s_local != 0u;
+    bool next_known = !p.l2local || j + 1 >= KM;   // lane 0: j + 1's XCD seen (or not needed)
+    auto look_next = [&]() {
+        const unsigned x = ld_agent(xccw + j + 1);
+        if (x != 0u) {
+            next_known = true;
+            s_local = x == my_xcc ? 1u : 0u;
+        }
+    };
+    if (tid == 0) {
+        s_local = 0u;
+        if (!next_known) look_next();
     }
 
     int t_prev = 0, pos_prev = 0, ch_prev = 0, pub_prev = 0;   // pub_prev: 0 none, 1 chain count, 2 fin word
@@ -1273,7 +1305,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
         if (i == 0 && tid == 0 && !(abl & 1)) {
-            if (pos > 0) wait_count(cnt + t, (unsigned)pos, serr, err, garr, stall);
+            if (pos > 0) wait_count(cnt + t, (unsigned)pos, serr, err, garr, prog, KM, stall);
             if (btail) s_direct[0] = ld_agent(fin + t) >= 1u ? 1u : 0u;
         }
         __syncthreads();
@@ -1331,7 +1363,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             const int tn = slice_of(i + 1);
             const Link ln = link_of(tn);
             if (tq == 0) {
-                if (ln.pos > 0) wait_count((ln.ch ? cnt1 : cnt0) + tn, (unsigned)ln.pos, serr, err, garr, stall);
+                if (!next_known) look_next();
+                if (ln.pos > 0) wait_count((ln.ch ? cnt1 : cnt0) + tn, (unsigned)ln.pos, serr, err, garr, prog, KM, stall);
                 if (ln.wrap && ln.ch == 1 && ln.pos == ln.len - 1)
                     s_direct[(i + 1) & 1] = ld_agent(fin + tn) >= 1u ? 1u : 0u;
             }
@@ -1347,8 +1380,10 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // by B2).  Read and waited for here: the dQ phase below counts its own LDS reads
         // by hand (lgkm_wait), so no compiler-issued LDS read may land among them.
         const unsigned dword = btail ? s_direct[i & 1] : 0u;
+        const unsigned lword = s_local;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const bool direct = btail && __builtin_amdgcn_readfirstlane(dword) != 0u;
+        const bool local = __builtin_amdgcn_readfirstlane(lword) != 0u;
         if (pub_prev && tid == 0) publish(t_prev, pos_prev, ch_prev, pub_prev);
 
         // next slice's images and row constants (land before the next B1)
@@ -1485,17 +1520,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 }
 
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
-// FA_HIP_BWD_SPLIT=1 in the environment selects the split passes for every call:
-// processes that share one GPU should, since the single pass needs every member of a
-// slab resident at once and a co-tenant's kernels hold the CUs it needs.
-static int env_bwd_mode() {
-    static const int m = [] {
-        const char* e = std::getenv("FA_HIP_BWD_SPLIT");
-        return (e != nullptr && e[0] == '1' && e[1] == '\0') ? 1 : 0;
-    }();
-    return m;
-}
-thread_local int g_bwd_mode = env_bwd_mode();   // 0 auto, 1 split passes, 2 single pass where the shape allows
+thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
 thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD
                                             // (-1 auto: at d, dv <= 64; 0 never; 1 always)
 thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members

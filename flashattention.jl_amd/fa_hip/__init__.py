@@ -37,7 +37,8 @@ import torch
 __all__ = [
     "DimensionMismatch", "FlashAttentionError", "lib", "lib_path",
     "jl_empty", "jl_zeros", "jl_tensor", "jl_strides", "is_jl_contiguous",
-    "dense_fa", "dense_fa_", "dense_fa_backward", "backward_handoff_status", "windowed_fa", "block_fa",
+    "dense_fa", "dense_fa_", "dense_fa_backward", "backward_handoff_status", "backward_handoff_trips",
+    "windowed_fa", "block_fa",
     "windowed_fa_backward", "window_geometry", "circulant_fa", "circulant_fa_", "circulant_dpa",
     "fused_softmax", "fused_softmax_", "DTYPES",
 ]
@@ -366,8 +367,8 @@ def fused_softmax(S: torch.Tensor, dims: int = 1) -> torch.Tensor:
 def dense_fa_backward(Q, K, V, O, dO, l, m, scale: float = 0.0):
     """``dense_fa_backward(Q, K, V, O, dO, l, m) -> (dQ, dK, dV)`` —
     src/dense.jl:104-167 (executable spec src_cpp/FlashAttention.cpp:194-252).
-    Processes that share one GPU should set ``FA_HIP_BWD_SPLIT=1`` before the library
-    loads: the single pass needs every member of a slab resident at once."""
+    The single-pass kernel needs no co-residency of a slab's workgroups, so calls on
+    several streams, or processes sharing one GPU, take it as well."""
     for t in (Q, K, V, O, dO, l, m):
         _require(t.dim() == 3, "dense_fa_backward expects 3-D (N, d, batch) arrays")
     N, d, B = Q.shape
@@ -395,9 +396,10 @@ def backward_handoff_status(device=None) -> int:
     on the current stream of ``device`` (its workspace is this module's per-stream
     scratch buffer).  Synchronises that stream.  -1: the two-pass form ran (no
     hand-off); 0: single pass, every dQ hand-off completed; 1: some slab's hand-off
-    gave up (its members could not all be resident: no arrival within 50 us, or a
-    20-ms bound) and that slab's dQ was recomputed by the guarded pass (same values
-    within rounding, other bits, slower).  Raises FlashAttentionError when no dense_fa_backward
+    gave up (the whole launch published nothing for 100 ms: a safety net, never
+    expected — every wait is on an earlier-dispatched workgroup) and that slab's dQ was
+    recomputed by the guarded pass (same values within rounding, other bits, slower).
+    Raises FlashAttentionError when no dense_fa_backward
     has run on this stream, or when another entry point has taken the scratch buffer
     since (the module records the last entry point per (device, stream))."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
@@ -410,6 +412,20 @@ def backward_handoff_status(device=None) -> int:
     _check(lib().fa_dense_bwd_handoff_status(_ptr(buf), buf.numel(), ctypes.c_void_p(stream.cuda_stream),
                                              ctypes.byref(st)))
     return int(st.value)
+
+
+def backward_handoff_trips(device=None) -> int:
+    """Slabs whose single-pass dQ hand-off gave up, counted over EVERY dense_fa_backward
+    that has used this stream's scratch buffer (a counter in the workspace header that
+    no call resets; it starts at whatever the buffer held, so read it before and after
+    a series of calls and take the difference).  Synchronises the stream."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    stream = torch.cuda.current_stream(device)
+    buf = _WS.get((device.type, device.index, stream.cuda_stream))
+    _require(buf is not None, "no scratch buffer on this stream yet")
+    off = ((buf.data_ptr() + 255) & ~255) - buf.data_ptr()
+    stream.synchronize()
+    return int(buf[off + 8:off + 12].view(torch.int32).item()) & 0xFFFFFFFF
 
 
 # ----------------------------------------------------------------------------

@@ -420,46 +420,3 @@ def test_backward_single_pass_multipass_grid_solo(fa, N, Nk, d, BH, xcd):
                                         _np(m[:, :, b:b + 1]))
     for a, r_, nm in zip(one, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
         assert_grad_close(sl(a), r_, "bfloat16", nm)
-
-
-_SPLIT_CHILD = r"""
-import os, sys, torch
-sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "flashattention.jl_amd")]
-import fa_hip as fa
-N, d, BH = 2048, 64, 64
-g = torch.Generator(device="cuda").manual_seed(5)
-mk = lambda: fa.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
-Q, K, V, dO = mk(), mk(), mk(), mk()
-Oo, l, m = fa.dense_fa(Q, K, V)
-out = fa.dense_fa_backward(Q, K, V, Oo, dO, l, m)
-torch.cuda.synchronize()
-torch.save({"status": fa.backward_handoff_status(), "grads": [t.cpu() for t in out]}, sys.argv[2])
-"""
-
-
-def test_backward_env_split_passes(fa, tmp_path):
-    """FA_HIP_BWD_SPLIT=1 (processes sharing a GPU): a configs-sized grid whose automatic
-    plan is the single pass runs the split passes instead, in a child process that
-    reads the variable at load; its gradients equal this process's split passes
-    bitwise (same seeded inputs)."""
-    import os, subprocess, sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    outs = {}
-    for env_val in ("1", None):
-        env = dict(os.environ)
-        env.pop("FA_HIP_BWD_SPLIT", None)
-        if env_val is not None:
-            env["FA_HIP_BWD_SPLIT"] = env_val
-        path = str(tmp_path / f"split_{env_val}.pt")
-        subprocess.run([sys.executable, "-c", _SPLIT_CHILD, root, path], env=env, check=True, timeout=110)
-        outs[env_val] = torch.load(path, weights_only=True)
-    assert outs["1"]["status"] == -1, outs["1"]["status"]
-    assert outs[None]["status"] == 0, outs[None]["status"]
-    N, d, BH = 2048, 64, 64
-    g = torch.Generator(device="cuda").manual_seed(5)
-    mk = lambda: fa.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
-    Q, K, V, dO = mk(), mk(), mk(), mk()
-    Oo, l, m = fa.dense_fa(Q, K, V)
-    split = _bwd_mode(fa, 1, Q, K, V, Oo, dO, l, m)
-    for a, b_, nm in zip(outs["1"]["grads"], split, ("dQ", "dK", "dV")):
-        assert torch.equal(a, b_.cpu()), nm + ": FA_HIP_BWD_SPLIT run differs from the split passes"

@@ -25,6 +25,9 @@ for p in paths:
     fa_hip._LIB = None
     os.environ["FA_HIP_LIB"] = os.path.abspath(p)
     libs.append(fa_hip.lib())
+    # AB_L2LOCAL=0/1: force the single pass's L2-local hand-off form in every build
+    if os.environ.get("AB_L2LOCAL") is not None and hasattr(libs[-1], "fa_debug_set_bwd_l2local"):
+        libs[-1].fa_debug_set_bwd_l2local(int(os.environ["AB_L2LOCAL"]))
 rounds = int(os.environ.get("AB_ROUNDS", 6))
 for (N, d, BH) in shapes:
     g = torch.Generator(device="cuda").manual_seed(1)
