@@ -1147,22 +1147,55 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     const u32x4 odesc = desc_of((const T*)p.dO + (int64_t)b * N * DV, (uint32_t)(N * DV * 2));
     // this wave's loop DMA ops per slice (dma_image8_asm), >= for every wave: a lower bound
     constexpr int NDMA = (D / 8 >= 8 ? D / 64 : 0) + (DV / 8 >= 8 ? DV / 64 : 0);
-    const FusedFlags ff = fused_flags(p.batch, NS, KM);
-    gu32* const cnt0 = (gu32*)(p.flags + ff.cnt + (int64_t)b * NS);               // chain A's per-slice counts
-    gu32* const cnt1 = (gu32*)(p.flags + ff.cnt + (int64_t)(p.batch + b) * NS);   // chain B's
-    gu32* const fin = (gu32*)(p.flags + ff.fin + (int64_t)b * NS);                // tails that stored (wrapped slices)
-    gu32* const err = (gu32*)p.err;
-    gu32* const serr = (gu32*)(p.flags + ff.serr + b);                            // this slab's trip word
-    gu32* const xccw = (gu32*)(p.flags + ff.xcc + (int64_t)b * KM);               // its members' XCDs + 1
-    gu32* const garr = (gu32*)(p.flags + ff.garr);                                // the launch's arrival count
-    gu32* const prog = (gu32*)(p.flags + ff.prog + (int64_t)b * KM);              // the slab's publish counts
-    gu32* const comb = (gu32*)(p.flags + ff.comb);
-    const uint64_t stall = (uint64_t)p.stall_ticks;
-    const unsigned my_xcc = (__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u) + 1u;   // HW_REG_XCC_ID[3:0]
+    // The hand-off's bookkeeping (polls, publishes, the XCD words) is lane 0's alone, so
+    // its pointers and state live in LDS, read where they are used through an address
+    // the compiler cannot see through (hc(): never hoisted into registers).  Held in
+    // SGPRs across the loop they spilled, and their v_readlane restores ran in every
+    // step of every wave (35 more SGPR spills than round 4's single chain, 4 times the
+    // restores in the loop, 6-13 % slower).
+    struct HoffCtx {
+        gu32* cnt[2];      // chains A, B: [NS] members of the chain that have published slice t
+        gu32* fin;         // [NS] tails of a wrapped slice's two chains that stored their sums
+        gu32* serr;        // this slab's trip word
+        gu32* err;         // the call's status word (err[1]: the sticky give-up count)
+        gu32* garr;        // the launch's arrival count
+        gu32* prog;        // [KM] the slab's publish progress
+        gu32* xccw;        // [KM] its members' XCDs + 1
+        gu32* comb;        // a wrapped slice is left to bwd_dq_fast's combine
+        uint64_t stall;    // no-progress bound of a poll
+        unsigned next_known;   // j + 1's XCD seen (or not needed)
+        unsigned pub;      // the last step's publish: kind | ch << 2 | pos << 3 | t << 12
+    };
+    __shared__ HoffCtx s_hc;
+    typedef __attribute__((address_space(3))) HoffCtx LHoff;
+    auto hc = [&]() {
+        uint32_t a = lds_addr(&s_hc);
+        asm volatile("" : "+v"(a));
+        return (LHoff*)(uintptr_t)a;
+    };
+    auto my_xcc = []() { return (__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u) + 1u; };   // HW_REG_XCC_ID[3:0]
     if (tid == 0) {
-        st_agent(xccw + j, my_xcc);
-        arrive(garr);
+        const FusedFlags ff = fused_flags(p.batch, NS, KM);
+        s_hc.cnt[0] = (gu32*)(p.flags + ff.cnt + (int64_t)b * NS);
+        s_hc.cnt[1] = (gu32*)(p.flags + ff.cnt + (int64_t)(p.batch + b) * NS);
+        s_hc.fin = (gu32*)(p.flags + ff.fin + (int64_t)b * NS);
+        s_hc.serr = (gu32*)(p.flags + ff.serr + b);
+        s_hc.err = (gu32*)p.err;
+        s_hc.garr = (gu32*)(p.flags + ff.garr);
+        s_hc.prog = (gu32*)(p.flags + ff.prog + (int64_t)b * KM);
+        s_hc.xccw = (gu32*)(p.flags + ff.xcc + (int64_t)b * KM);
+        s_hc.comb = (gu32*)(p.flags + ff.comb);
+        s_hc.stall = (uint64_t)p.stall_ticks;
+        s_hc.next_known = (!p.l2local || j + 1 >= KM) ? 1u : 0u;
+        s_hc.pub = 0u;
+        st_agent(s_hc.xccw + j, my_xcc());
+        arrive(s_hc.garr);
     }
+    // lane 0: wait until chain ch's member pos - 1 has published slice t
+    auto poll = [&](int ch, int t, int pos) {
+        LHoff* const h = hc();
+        wait_count(h->cnt[ch] + t, (unsigned)pos, h->serr, h->err, h->garr, h->prog, KM, h->stall);
+    };
 
     const int g = lane >> 4, kh = g & 1, qq = (lane & 15) >> 2, pp = lane & 3;
     const int sig = (pp == 1) ? 2 : (pp == 2) ? 1 : pp;
@@ -1196,8 +1229,35 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         int ch, pos, len;
         bool wrap;
     };
-    auto link_of = [&](int t) {
-        const int w0 = (NS - t + OFF - 1) / OFF;
+    // Walked without divisions (a runtime % NS and / OFF per use cost ~50 SALU
+    // instructions each, in every wave): the step's slice t and w0 = ceil((NS − t)/OFF)
+    // as w0 and r0 = NS − t − (w0 − 1)·OFF in [1, OFF], advanced by one slice per step.
+    struct Walk {
+        int t, w0, r0;
+    };
+    const int w0_at0 = (NS + OFF - 1) / OFF, r0_at0 = NS - (w0_at0 - 1) * OFF;   // slice 0
+    auto walk_at = [&](int t) {
+        Walk s;
+        s.t = t;
+        s.w0 = (NS - t + OFF - 1) / OFF;
+        s.r0 = NS - t - (s.w0 - 1) * OFF;
+        return s;
+    };
+    auto advance = [&](const Walk& s) {
+        Walk n;
+        if (s.t + 1 == NS) {
+            n.t = 0;
+            n.w0 = w0_at0;
+            n.r0 = r0_at0;
+        } else {
+            n.t = s.t + 1;
+            n.w0 = s.r0 == 1 ? s.w0 - 1 : s.w0;
+            n.r0 = s.r0 == 1 ? OFF : s.r0 - 1;
+        }
+        return n;
+    };
+    auto link_of = [&](const Walk& s) {
+        const int w0 = s.w0;
         Link L;
         L.wrap = w0 < KM;
         L.ch = L.wrap && j < w0 ? 1 : 0;
@@ -1210,16 +1270,25 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     // atomic would make this wave wait for the step's running-sum loads).  fin == 2
     // after the launch means both tails stored their totals: chain B's tail found A
     // unfinished, stored instead of writing dQ, and flagged the launch (comb) so that
-    // bwd_dq_fast adds them.  Every publish counts as progress of the slab (prog).
-    unsigned npub = 0;
-    auto publish = [&](int tp, int posp, int chp, int kind) {
+    // bwd_dq_fast adds them.  Every publish counts as progress of the slab: prog[j] takes
+    // the number of steps done, which grows with every publish (lane 0, s_hc.pub).
+    auto publish = [&](unsigned steps) {
+        // every word read at once (one LDS round trip on wave 0 after B2, not a chain)
+        LHoff* const h = hc();
+        const unsigned pk = h->pub;
+        gu32* const c0 = h->cnt[0];
+        gu32* const c1 = h->cnt[1];
+        gu32* const fn = h->fin;
+        gu32* const cm = h->comb;
+        gu32* const pg = h->prog;
+        const int kind = pk & 3u, chp = (pk >> 2) & 1u, posp = (pk >> 3) & 511u, tp = pk >> 12;
         if (kind == 1) {
-            st_agent((chp ? cnt1 : cnt0) + tp, (unsigned)(posp + 1));
-        } else {
-            __hip_atomic_fetch_add(fin + tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (chp == 1) st_agent(comb, 1u);
+            st_agent((chp ? c1 : c0) + tp, (unsigned)(posp + 1));
+        } else if (kind == 2) {
+            __hip_atomic_fetch_add(fn + tp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (chp == 1) st_agent(cm, 1u);
         }
-        st_agent(prog + j, (unsigned)++npub);
+        if (kind != 0) st_agent(pg + j, steps);
     };
     auto load_rowc = [&](int t) {
         const int q = t * 64 + (tid & 63);
@@ -1230,7 +1299,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     };
 
     // ---- prologue: K images (once), the first slice, V fragments of this lane's key ----
-    int t = slice_of(0);
+    Walk cur = walk_at(slice_of(0));
+    int t = cur.t;
     {
         const float rc = load_rowc(t);
 #pragma unroll
@@ -1272,25 +1342,26 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     // else.  A chain's tail stores sc1 always.
     __shared__ unsigned s_local;       // read after B2 of each step
     __shared__ unsigned s_direct[2];   // chain B's tail of step i's slice: A had finished (slot i & 1)
-    bool next_known = !p.l2local || j + 1 >= KM;   // lane 0: j + 1's XCD seen (or not needed)
-    auto look_next = [&]() {
-        const unsigned x = ld_agent(xccw + j + 1);
+    auto look_next = [&]() {           // lane 0
+        LHoff* const h = hc();
+        if (h->next_known) return;
+        const unsigned x = ld_agent(h->xccw + j + 1);
         if (x != 0u) {
-            next_known = true;
-            s_local = x == my_xcc ? 1u : 0u;
+            h->next_known = 1u;
+            s_local = x == my_xcc() ? 1u : 0u;
         }
     };
     if (tid == 0) {
         s_local = 0u;
-        if (!next_known) look_next();
+        look_next();
     }
 
-    int t_prev = 0, pos_prev = 0, ch_prev = 0, pub_prev = 0;   // pub_prev: 0 none, 1 chain count, 2 fin word
+    bool pub_prev = false;   // the last step left a publish for lane 0 (kind in s_hc.pub)
     for (int i = 0; i < NS; ++i) {
-        t = slice_of(i);
-        const Link lk = link_of(t);
+        t = cur.t;
+        const Link lk = link_of(cur);
+        const Walk nxt = advance(cur);
         const int pos = lk.pos;
-        gu32* const cnt = lk.ch ? cnt1 : cnt0;
         const int tq = opaque(tid), lq = tq & 63, rq = lq & 31, hq = lq >> 5;   // re-derived per step
         const bool tail = pos == lk.len - 1;
         const bool btail = lk.wrap && tail && lk.ch == 1;   // chain B's tail: makes A + B when A is done
@@ -1305,8 +1376,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
         if (i == 0 && tid == 0 && !(abl & 1)) {
-            if (pos > 0) wait_count(cnt + t, (unsigned)pos, serr, err, garr, prog, KM, stall);
-            if (btail) s_direct[0] = ld_agent(fin + t) >= 1u ? 1u : 0u;
+            if (pos > 0) poll(lk.ch, t, pos);
+            if (btail) s_direct[0] = ld_agent(hc()->fin + t) >= 1u ? 1u : 0u;
         }
         __syncthreads();
 
@@ -1360,13 +1431,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // (drained in the middle of this phase), so the poll pays only its own latency,
         // and barriers B2 and B1 order it before every wave's sum loads of that step
         if (wave == 0 && i + 1 < NS && !(abl & 1)) {
-            const int tn = slice_of(i + 1);
-            const Link ln = link_of(tn);
+            const int tn = nxt.t;
+            const Link ln = link_of(nxt);
             if (tq == 0) {
-                if (!next_known) look_next();
-                if (ln.pos > 0) wait_count((ln.ch ? cnt1 : cnt0) + tn, (unsigned)ln.pos, serr, err, garr, prog, KM, stall);
+                look_next();
+                if (ln.pos > 0) poll(ln.ch, tn, ln.pos);
                 if (ln.wrap && ln.ch == 1 && ln.pos == ln.len - 1)
-                    s_direct[(i + 1) & 1] = ld_agent(fin + tn) >= 1u ? 1u : 0u;
+                    s_direct[(i + 1) & 1] = ld_agent(hc()->fin + tn) >= 1u ? 1u : 0u;
             }
         }
         if (has_tile && !(abl & 10)) {
@@ -1384,14 +1455,14 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const bool direct = btail && __builtin_amdgcn_readfirstlane(dword) != 0u;
         const bool local = __builtin_amdgcn_readfirstlane(lword) != 0u;
-        if (pub_prev && tid == 0) publish(t_prev, pos_prev, ch_prev, pub_prev);
+        if (pub_prev && tid == 0) publish((unsigned)i);
 
         // next slice's images and row constants (land before the next B1)
         // (the last step reloads its own slice: harmless, nothing reads it)
         float rc;
         bool rc_in;
         {
-            const int tn = i + 1 < NS ? slice_of(i + 1) : t;
+            const int tn = i + 1 < NS ? nxt.t : t;
             const int q = tn * 64 + lq;
             rc = load4_asm((tq < 64 ? nlse : nDg) + (q < N ? q : N - 1));   // asm: counted below
             rc_in = q < N;
@@ -1490,15 +1561,16 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 }
             }
         }
-        t_prev = t;
-        pos_prev = pos;
-        ch_prev = lk.ch;
-        pub_prev = (tail && !lk.wrap) || direct ? 0 : tail ? 2 : 1;
+        // publish kind: 0 none (dQ written), 1 chain count, 2 fin word (a wrapped chain's tail)
+        const unsigned kind = (tail && !lk.wrap) || direct ? 0u : tail ? 2u : 1u;
+        pub_prev = kind != 0u;
+        if (tid == 0) hc()->pub = kind | (unsigned)lk.ch << 2 | (unsigned)pos << 3 | (unsigned)t << 12;
+        cur = nxt;
     }
     if (pub_prev) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) publish(t_prev, pos_prev, ch_prev, pub_prev);
+        if (tid == 0) publish((unsigned)NS);
     }
     if (key_ok) {
         const auto ko = bslab<T>(p.dK, (int64_t)b * Nk * D, (int64_t)Nk * D);

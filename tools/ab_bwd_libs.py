@@ -25,6 +25,9 @@ for p in paths:
     fa_hip._LIB = None
     os.environ["FA_HIP_LIB"] = os.path.abspath(p)
     libs.append(fa_hip.lib())
+    # AB_MODE=m: fa_debug_set_bwd_mode(m) in every build (4.. = timing-only ablations of -DFA_BWD_ABL builds)
+    if os.environ.get("AB_MODE") is not None:
+        libs[-1].fa_debug_set_bwd_mode(int(os.environ["AB_MODE"]))
     # AB_L2LOCAL=0/1: force the single pass's L2-local hand-off form in every build
     if os.environ.get("AB_L2LOCAL") is not None and hasattr(libs[-1], "fa_debug_set_bwd_l2local"):
         libs[-1].fa_debug_set_bwd_l2local(int(os.environ["AB_L2LOCAL"]))

@@ -2,6 +2,7 @@
 # Build a copy of libfa_hip.so with extra flags on fa_bwd.hip (A/B builds):
 #   tools/exp/build_bwd_variant.sh OUT.so "-mllvm ... -DFOO=1"
 set -e
+[ -n "$1" ] || { echo "usage: $0 OUT.so \"flags\"" >&2; exit 2; }
 C=/root/repo/flashattention.jl_amd/csrc
 B=/tmp/bwdvar_$$
 mkdir -p $B
