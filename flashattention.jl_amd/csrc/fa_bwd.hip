@@ -1072,7 +1072,9 @@ __device__ __forceinline__ void dma16_asm(const u32x4& desc, uint32_t lds_base, 
 template <int OFF>
 __device__ __forceinline__ u32x4 load16_sc1_asm(const u32x4& desc, int voff) {
     u32x4 r;
-    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 sc1" : "=v"(r) : "v"(voff), "s"(desc), "i"(OFF) : "memory");
+    // no s_nop here: no spill restore lands in front of these (tools/vmem_sgpr_hazards.py,
+    // tests/test_code_hazards.py); one per load cost 2 % at configs[3]
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 sc1" : "=v"(r) : "v"(voff), "s"(desc), "i"(OFF) : "memory");
     return r;
 }
 // dma_image8 through dma16_asm; returns nothing, issues (R/8 + 7)/8 ops or fewer per wave

@@ -1,0 +1,40 @@
+"""The built gfx950 code object has no VALU-writes-SGPR -> vector-memory-reads-SGPR
+hazard closer than the 5 wait states the ISA requires (tools/vmem_sgpr_hazards.py).
+The compiler's hazard recognizer inserts those wait states for the instructions it
+emits, not in front of inline asm: fa_bwd.hip's asm LDS-DMA loads carry an `s_nop 4`
+(a spilled descriptor restored by v_readlane right before one gave wrong dQ/dK/dV at
+d = 32), and its asm running-sum loads carry none, which this test keeps honest for
+whatever the compiler's register allocation does.  CPU only: it reads the library."""
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+LIB = os.path.join(ROOT, "flashattention.jl_amd", "libfa_hip.so")
+
+
+def test_no_valu_sgpr_vmem_hazards():
+    import vmem_sgpr_hazards as H
+    if not os.path.exists(LIB):
+        pytest.skip("libfa_hip.so not built")
+    if shutil.which("objcopy") is None or not os.path.exists(os.path.join(H.LLVM, "llvm-objdump")):
+        pytest.skip("binutils / ROCm llvm tools missing")
+    lines = H.disassemble(LIB)
+    assert sum(1 for l in lines if "offen lds" in l) > 100, "the DMA kernels were not found in the disassembly"
+    found = H.scan(lines)
+    assert not found, "\n".join(f"{f}: {a} -> {b} ({ws} wait states)" for f, a, b, ws in found[:10])
+
+
+def test_checker_sees_a_planted_hazard():
+    import vmem_sgpr_hazards as H
+    lines = ["0000000000001000 <k>:",
+             "\tv_readlane_b32 s87, v161, 14  // 0",
+             "\tbuffer_load_dwordx4 v50, s[84:87], 0 offen lds  // 0",
+             "\tv_readlane_b32 s3, v1, 0",
+             "\ts_nop 4",
+             "\tbuffer_load_dwordx4 v[0:3], v2, s[0:3], 0 offen offset:16 sc1"]
+    found = H.scan(lines)
+    assert len(found) == 1 and found[0][1].startswith("v_readlane_b32 s87")
