@@ -1437,9 +1437,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             const Link ln = link_of(nxt);
             if (tq == 0) {
                 look_next();
+                // a chain-B tail reads chain A's fin word with its poll (one round
+                // trip for both; read again if A was not done then)
+                const bool bt = ln.wrap && ln.ch == 1 && ln.pos == ln.len - 1;
+                gu32* const fw = hc()->fin + tn;
+                const unsigned f0 = bt ? ld_agent(fw) : 0u;
                 if (ln.pos > 0) poll(ln.ch, tn, ln.pos);
-                if (ln.wrap && ln.ch == 1 && ln.pos == ln.len - 1)
-                    s_direct[(i + 1) & 1] = ld_agent(hc()->fin + tn) >= 1u ? 1u : 0u;
+                if (bt) s_direct[(i + 1) & 1] = f0 >= 1u || ld_agent(fw) >= 1u ? 1u : 0u;
             }
         }
         if (has_tile && !(abl & 10)) {
@@ -1447,6 +1451,20 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             pin[1] = load16_sc1_asm<1024>(pdesc, pofs);
             pin[2] = load16_sc1_asm<2048>(pdesc, pofs);
             pin[3] = load16_sc1_asm<3072>(pdesc, pofs);
+        }
+        // a chain-B tail at d, dv <= 64 loads chain A's total here too, before it knows
+        // (after B2) whether A had finished at its poll: used only if it had (then the
+        // poll, earlier in program order, saw A's publish, which follows A's stores),
+        // and counted with the running sum (vm_wait<NDMA>).  At 128 its 16 registers
+        // would spill across the dQ phase: loaded after that phase instead.
+        constexpr bool kPrefA = D <= 64 && DV <= 64;
+        u32x4 pa[4];
+        if (kPrefA && has_tile && btail && !(abl & 10)) {
+            const int pofa = pofs - pchain4;
+            pa[0] = load16_sc1_asm<0>(pdesc, pofa);
+            pa[1] = load16_sc1_asm<1024>(pdesc, pofa);
+            pa[2] = load16_sc1_asm<2048>(pdesc, pofa);
+            pa[3] = load16_sc1_asm<3072>(pdesc, pofa);
         }
         __syncthreads();   // B2: dSᵀ complete, the slice's images free, last step's sums stored
         // chain B's tail: whether A's total was there at the poll (lane 0's word, ordered
@@ -1531,17 +1549,19 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             // chain B's tail with A finished: A's total (its tail's sc1 stores, published
             // through fin before this step's poll) in, after this chain's own sum
             if (direct) {
-                const int pofa = pofs - pchain4;
-                pin[0] = load16_sc1_asm<0>(pdesc, pofa);
-                pin[1] = load16_sc1_asm<1024>(pdesc, pofa);
-                pin[2] = load16_sc1_asm<2048>(pdesc, pofa);
-                pin[3] = load16_sc1_asm<3072>(pdesc, pofa);
-                vm_wait<0>();
+                if constexpr (!kPrefA) {
+                    const int pofa = pofs - pchain4;
+                    pa[0] = load16_sc1_asm<0>(pdesc, pofa);
+                    pa[1] = load16_sc1_asm<1024>(pdesc, pofa);
+                    pa[2] = load16_sc1_asm<2048>(pdesc, pofa);
+                    pa[3] = load16_sc1_asm<3072>(pdesc, pofa);
+                    vm_wait<0>();
+                }
 #pragma unroll
                 for (int c4 = 0; c4 < 4; ++c4) {
-                    reg_fence(pin[c4]);
+                    reg_fence(pa[c4]);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pin[c4][e]);
+                    for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pa[c4][e]);
                 }
             }
             if ((tail && !lk.wrap) || direct) {
