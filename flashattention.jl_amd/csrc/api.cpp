@@ -193,6 +193,17 @@ int fa_debug_set_bwd_stall_us(int v) {
     return old;
 }
 
+// Not part of the public header (tests): 1 makes every chain-B tail of the single-pass
+// backward store its total and leave dQ = A + B of the wrapped slices to the guarded dQ
+// pass's combine (the path a co-tenant can force), 0 the default; returns the previous
+// value (-2 for an invalid argument).
+int fa_debug_set_bwd_nodirect(int v) {
+    const int old = fa::g_bwd_nodirect;
+    if (v < 0 || v > 1) return -2;
+    fa::g_bwd_nodirect = v;
+    return old;
+}
+
 // Not part of the public header: circulant kernel override (1 one-wave-per-query,
 // 2 LDS-tiled SIMT; 0 auto).
 int fa_debug_set_circ_generic(int v) {

@@ -41,8 +41,7 @@ struct FusedFlags {
     int64_t xcc;    // [batch][KM]: XCD of each member + 1 (L2-local hand-off)
     int64_t prog;   // [batch][KM]: each member's count of publishes (plain stores, no contention)
     int64_t garr;   // the launch's arrival count (one add per workgroup)
-    int64_t comb;   // a wrapped slice is left to bwd_dq_fast's combine
-    int64_t words;
+    int64_t words;  // (a wrapped slice left to bwd_dq_fast's combine is flagged in hdr[3])
 };
 __host__ __device__ inline FusedFlags fused_flags(int64_t batch, int64_t NS, int64_t KM) {
     FusedFlags f;
@@ -52,8 +51,7 @@ __host__ __device__ inline FusedFlags fused_flags(int64_t batch, int64_t NS, int
     f.xcc = f.serr + batch;
     f.prog = f.xcc + batch * KM;
     f.garr = f.prog + batch * KM;
-    f.comb = f.garr + 1;
-    f.words = f.comb + 1;
+    f.words = f.garr + 1;
     return f;
 }
 
@@ -72,12 +70,14 @@ struct BwdParams {
     unsigned* err = nullptr;     // hand-off timeout word = hdr[1] (set per call by the pre-pass)
     // workspace header (first 256 B of the aligned workspace; fa_dense_bwd_handoff_status):
     // hdr[0] = kBwdHdrMagic | plan (1 = single pass), hdr[1] = the timeout word,
-    // hdr[2] = give-ups counted over every call on this workspace (never reset here)
+    // hdr[2] = give-ups counted over every call on this workspace (never reset here),
+    // hdr[3] = some chain-B tail of this call left its slice to bwd_dq_fast's combine
     unsigned* hdr = nullptr;
     unsigned hdr_plan = 0, hdr_err = 0;
     float* part = nullptr;       // [batch][2 chains][nqt][D/16 tiles][16 x 64] fp32 running dQ sums
     int nkb = 0, nqt = 0, hoff = 3, xcd = 0;   // key blocks, 64-query slices, step offset, XCD mapping
     int stall_ticks = kStallUs * 100;   // no-progress bound of a poll in s_memrealtime ticks (100 MHz)
+    int nodirect = 0;                   // tests: chain-B tails store, bwd_dq_fast adds A + B (fa_debug_set_bwd_nodirect)
     int l2local = 0;  // 1: hand the running sums over in the XCD's L2 when a slab's members share one
     int ablate = 0;   // timing-only ablations (wrong dQ): 1 no waits, 2 no sum traffic, 8 no sum loads, 16 no sum stores, 32 no dS image writes
     const unsigned* guard = nullptr;           // bwd_dq_fast runs only if *guard != 0 (nullptr: always)
@@ -97,6 +97,7 @@ __device__ __forceinline__ void write_bwd_header(const BwdParams& p) {
     if (p.hdr) {
         p.hdr[0] = kBwdHdrMagic | p.hdr_plan;
         p.hdr[1] = p.hdr_err;
+        p.hdr[3] = 0u;   // set by a chain-B tail that left its slice to the combine (read by tests)
     }
 }
 
@@ -1167,6 +1168,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         uint64_t stall;    // no-progress bound of a poll
         unsigned next_known;   // j + 1's XCD seen (or not needed)
         unsigned pub;      // the last step's publish: kind | ch << 2 | pos << 3 | t << 12
+        unsigned nodirect; // tests: a chain-B tail never takes the direct add (p.nodirect)
     };
     __shared__ HoffCtx s_hc;
     typedef __attribute__((address_space(3))) HoffCtx LHoff;
@@ -1186,10 +1188,11 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         s_hc.garr = (gu32*)(p.flags + ff.garr);
         s_hc.prog = (gu32*)(p.flags + ff.prog + (int64_t)b * KM);
         s_hc.xccw = (gu32*)(p.flags + ff.xcc + (int64_t)b * KM);
-        s_hc.comb = (gu32*)(p.flags + ff.comb);
+        s_hc.comb = (gu32*)(p.hdr + 3);
         s_hc.stall = (uint64_t)p.stall_ticks;
         s_hc.next_known = (!p.l2local || j + 1 >= KM) ? 1u : 0u;
         s_hc.pub = 0u;
+        s_hc.nodirect = p.nodirect ? 1u : 0u;
         st_agent(s_hc.xccw + j, my_xcc());
         arrive(s_hc.garr);
     }
@@ -1379,7 +1382,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
         if (i == 0 && tid == 0 && !(abl & 1)) {
             if (pos > 0) poll(lk.ch, t, pos);
-            if (btail) s_direct[0] = ld_agent(hc()->fin + t) >= 1u ? 1u : 0u;
+            if (btail) s_direct[0] = !hc()->nodirect && ld_agent(hc()->fin + t) >= 1u ? 1u : 0u;
         }
         __syncthreads();
 
@@ -1443,7 +1446,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 gu32* const fw = hc()->fin + tn;
                 const unsigned f0 = bt ? ld_agent(fw) : 0u;
                 if (ln.pos > 0) poll(ln.ch, tn, ln.pos);
-                if (bt) s_direct[(i + 1) & 1] = f0 >= 1u || ld_agent(fw) >= 1u ? 1u : 0u;
+                if (bt) s_direct[(i + 1) & 1] = !hc()->nodirect && (f0 >= 1u || ld_agent(fw) >= 1u) ? 1u : 0u;
             }
         }
         if (has_tile && !(abl & 10)) {
@@ -1619,6 +1622,7 @@ thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when
                                             // (-1 auto: at d, dv <= 64; 0 never; 1 always)
 thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between consecutive members
 thread_local int g_bwd_stall_us = kStallUs; // bwd_fused: no-progress bound of a poll (us)
+thread_local int g_bwd_nodirect = 0;         // bwd_fused (tests): every wrapped slice left to bwd_dq_fast's combine
 thread_local int g_bwd_xcd = -1;            // bwd_fused: one XCD per slab where eligible (-1 auto, 0 never)
 
 template <class T, int D, int DV>
@@ -1630,7 +1634,7 @@ static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
         const FusedFlags ff = fused_flags(p.batch, p.nqt, p.nkb);
         p.guard = p.err;
         p.sguard = p.flags + ff.serr;
-        p.cguard = p.flags + ff.comb;
+        p.cguard = p.hdr + 3;
         p.fin = p.flags + ff.fin;
     }
     p.nblk = (p.N + 127) / 128;
@@ -1850,6 +1854,7 @@ static hipError_t fused_setup(BwdParams& p, const FusedPlan& fz, char* w, hipStr
     p.l2local = g_bwd_l2local >= 0 ? g_bwd_l2local : (p.d <= 64 && p.dv <= 64 ? 1 : 0);
     p.hoff = g_bwd_hoff;
     p.stall_ticks = g_bwd_stall_us * 100;
+    p.nodirect = g_bwd_nodirect;
 #ifdef FA_BWD_ABL
     p.ablate = g_bwd_mode == 7 ? 8 : g_bwd_mode == 8 ? 16 : g_bwd_mode == 9 ? 32 : g_bwd_mode == 10 ? 64
              : g_bwd_mode == 11 ? 64 | 3 : g_bwd_mode >= 4 ? g_bwd_mode - 3 : 0;

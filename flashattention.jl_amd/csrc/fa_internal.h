@@ -146,7 +146,8 @@ extern thread_local int g_bwd_force_generic;  // backward: force the generic SIM
 extern thread_local int g_bwd_mode;           // backward MFMA path: 0 auto, 1 split passes, 2 single pass
 extern thread_local int g_bwd_l2local;        // single pass: running sums handed over in the XCD's L2
 extern thread_local int g_bwd_hoff;           // single pass: step offset between consecutive members
-extern thread_local int g_bwd_stall_us;       // single pass: residency-check window (us)
+extern thread_local int g_bwd_stall_us;       // single pass: no-progress bound of a poll (us)
+extern thread_local int g_bwd_nodirect;       // single pass (tests): chain-B tails never add A's total themselves
 extern thread_local int g_bwd_xcd;            // single pass: one XCD per slab where eligible (-1 auto, 0 never)
 extern thread_local int g_win_force_composed; // windowed: forced path (composed / fused variants)
 extern thread_local int g_circ_force_generic; // circulant: forced kernel

@@ -419,13 +419,20 @@ def backward_handoff_trips(device=None) -> int:
     that has used this stream's scratch buffer (a counter in the workspace header that
     no call resets; it starts at whatever the buffer held, so read it before and after
     a series of calls and take the difference).  Synchronises the stream."""
+    return _backward_header_word(2, device)
+
+
+def _backward_header_word(i: int, device=None) -> int:
+    """Word i of the fa_dense_bwd workspace header on this stream's scratch buffer
+    (2: the sticky give-up count; 3: the last call left some wrapped slice's A + B to
+    the guarded dQ pass — tests).  Synchronises the stream."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     stream = torch.cuda.current_stream(device)
     buf = _WS.get((device.type, device.index, stream.cuda_stream))
     _require(buf is not None, "no scratch buffer on this stream yet")
-    off = ((buf.data_ptr() + 255) & ~255) - buf.data_ptr()
+    off = ((buf.data_ptr() + 255) & ~255) - buf.data_ptr() + 4 * i
     stream.synchronize()
-    return int(buf[off + 8:off + 12].view(torch.int32).item()) & 0xFFFFFFFF
+    return int(buf[off:off + 4].view(torch.int32).item()) & 0xFFFFFFFF
 
 
 # ----------------------------------------------------------------------------

@@ -420,3 +420,42 @@ def test_backward_single_pass_multipass_grid_solo(fa, N, Nk, d, BH, xcd):
                                         _np(m[:, :, b:b + 1]))
     for a, r_, nm in zip(one, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
         assert_grad_close(sl(a), r_, "bfloat16", nm)
+
+
+@pytest.mark.parametrize("N,Nk,d,dv,BH", [(2048, 2048, 64, 64, 64), (4096, 2048, 128, 128, 32),
+                                          (1024, 768, 128, 64, 40)])
+def test_backward_chain_b_combine_bitwise(fa, N, Nk, d, dv, BH):
+    """Where a slice's member order wraps it runs as two chains, and dQ = A + B is made
+    either by chain B's tail (A done at its poll: every slice of a solo call) or, when
+    A finished later, by the guarded dQ pass after the launch (fused_combine) — the
+    path a co-tenant can force on any slice.  Forced for every wrapped slice
+    (fa_debug_set_bwd_nodirect), it must give the same bits, since it is the same single
+    fp32 add; header word 3 shows the combine ran."""
+    import ctypes
+    L = fa.lib()
+    L.fa_debug_set_bwd_nodirect.restype = ctypes.c_int
+    g = torch.Generator(device="cuda").manual_seed(N + d + BH)
+    mk = lambda n, c: fa.jl_tensor(torch.randn((n, c, BH), generator=g, device="cuda"), torch.bfloat16)
+    Q, K, V, dO = mk(N, d), mk(Nk, d), mk(Nk, dv), mk(N, dv)
+    Oo, l, m = fa.dense_fa(Q, K, V)
+    st, comb = [], []
+    old = L.fa_debug_set_bwd_nodirect(1)
+    assert old == 0
+    try:
+        forced = [t.clone() for t in _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m, status=st)]
+        comb.append(fa._backward_header_word(3))
+    finally:
+        assert L.fa_debug_set_bwd_nodirect(old) == 1
+    assert L.fa_debug_set_bwd_nodirect(2) == -2
+    direct = [t.clone() for t in _bwd_mode(fa, 2, Q, K, V, Oo, dO, l, m, status=st)]
+    comb.append(fa._backward_header_word(3))
+    assert st == [0, 0], st
+    assert comb[0] == 1, "the forced run never reached the combine"
+    for a, b_, nm in zip(forced, direct, ("dQ", "dK", "dV")):
+        assert torch.equal(a, b_), nm + ": combine in the dQ pass not bitwise equal to chain B's direct add"
+    b = BH // 2
+    sl = lambda t: _np(t[:, :, b:b + 1])
+    dqr, dkr, dvr = O.dense_fa_backward(sl(Q), sl(K), sl(V), sl(Oo), sl(dO), _np(l[:, :, b:b + 1]),
+                                        _np(m[:, :, b:b + 1]))
+    for a, r_, nm in zip(forced, (dqr, dkr, dvr), ("dQ", "dK", "dV")):
+        assert_grad_close(sl(a), r_, "bfloat16", nm)
