@@ -1305,12 +1305,14 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
 // backward: 20 ms at B = 32).
 //
 //   staging  : q, k, v, dy rows by the row-shift loads of the forward kernel into
-//              [feature][slot] images (128-B swizzled rows); y rows only feed
-//              D = rowsum(dy ∘ y), accumulated per slot with LDS float adds.
+//              [feature][slot] images (128-B swizzled rows).  y is not read (round 5:
+//              a fifth of the loads, on CUs that run two windows at B = 1).
 //   phase 1  : wave (qb, kb) computes the 32x32 blocks S = Q Kᵀ and dP = dO Vᵀ
-//              (queries on accumulator rows, keys on lanes) with −lse/τ and −D as
-//              the initial accumulators, P = exp2(c·S'), dS = P ∘ (dP − D), and
-//              writes P, dS (bf16) into [key][query] images (144-B rows).
+//              (queries on accumulator rows, keys on lanes) with −lse/τ as S's
+//              initial accumulator, P = exp2(c·S'), and D = rowsum(P ∘ dP) (= rowsum
+//              (dy ∘ y)): each wave's 32-key partial by DPP / permlane16 sums within
+//              its lane halves, the two key halves' partials added through LDS; then
+//              dS = P ∘ (dP − D), and P, dS (bf16) go into [key][query] images (144-B rows).
 //   phase 2  : 12 blocks over the 4 waves: dVᵀ = dOᵀ P, dKᵀ = τ Qᵀ dS (row
 //              reads), dQᵀ = τ Kᵀ dSᵀ (dSᵀ by transposed reads of the [key][query]
 //              image); each lane stores one slot's features straight to its pixel.
@@ -1334,7 +1336,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     __shared__ __attribute__((aligned(16))) char smem[REGION];
     auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
     float* const lse_s = (float*)(smem + OLSE);   // −lse/τ per query slot (raw score units)
-    float* const dsum = (float*)(smem + OD);      // D per query slot: one partial per wave [4][64]
+    float* const dsum = (float*)(smem + OD);      // D per query slot: one partial per key half [2][64]
 
     FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -1355,9 +1357,9 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
     const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
     const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
-    const auto yrs = slab_rsrc(y + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    (void)y;
     const auto drs = slab_rsrc(dy + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
-    u32x4 rq[NIQ], rk[NIQ], rv[NIV], ry[NIV], rd[NIV];
+    u32x4 rq[NIQ], rk[NIQ], rv[NIV], rd[NIV];
 #pragma unroll
     for (int j = 0; j < NIQ; ++j) {
         const int o = item_off(tid + NTH * j, d);
@@ -1369,7 +1371,6 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         const int o = item_off(tid + NTH * j, dv);
         rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, o, 0, 0);
         rd[j] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
-        ry[j] = __builtin_amdgcn_raw_buffer_load_b128(yrs, o, 0, 0);
     }
     // per-slot constant −lse/τ (+inf lse outside the window)
     if (tid < 64) {
@@ -1400,38 +1401,11 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         *(u32x4*)(smem + OK_ + o) = shift_row(rk[j], sh, mask);
     }
     FA_STAMP(1);
-    // D = rowsum(dy ∘ y) per slot.  Lane (8·fl + yy) of wave w holds window row yy of
-    // features 8w + 32j + fl: sum over j in registers, over fl (lane bits 3..5) by
-    // row_ror:8 + permlane16/32 swaps, then lanes 0..7 write the wave's partial for
-    // the 8 slots of their row (no LDS atomics: same-address adds serialise).
-    float dp[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dp[e] = 0.0f;
 #pragma unroll
     for (int j = 0; j < NIV; ++j) {
-        const int it = tid + NTH * j, o = koff(it);
-        const u32x4 dd = shift_row(rd[j], sh, mask), yv = shift_row(ry[j], sh, mask);
+        const int o = koff(tid + NTH * j);
         *(u32x4*)(smem + OV + o) = shift_row(rv[j], sh, mask);
-        *(u32x4*)(smem + ODO + o) = dd;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const unsigned short a16 = (unsigned short)((e & 1) ? (dd[e >> 1] >> 16) : (dd[e >> 1] & 0xFFFFu));
-            const unsigned short b16 = (unsigned short)((e & 1) ? (yv[e >> 1] >> 16) : (yv[e >> 1] & 0xFFFFu));
-            dp[e] = fmaf((float)__builtin_bit_cast(T, a16), (float)__builtin_bit_cast(T, b16), dp[e]);
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        float x = dp[e];
-        x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
-        auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-        x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
-        auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-        dp[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-    }
-    if (lane < 8) {
-        *(f32x4*)(dsum + wave * 64 + lane * 8) = f32x4{dp[0], dp[1], dp[2], dp[3]};
-        *(f32x4*)(dsum + wave * 64 + lane * 8 + 4) = f32x4{dp[4], dp[5], dp[6], dp[7]};
+        *(u32x4*)(smem + ODO + o) = shift_row(rd[j], sh, mask);
     }
     __syncthreads();
     FA_STAMP(2);
@@ -1449,12 +1423,9 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     f32x16 sa, pa;
 #pragma unroll
     for (int x4 = 0; x4 < 4; ++x4) {
-        const int qrow = qb * 32 + acc_row(4 * x4, h);
-        const f32x4 l4 = *(const f32x4*)(lse_s + qrow);
-        const f32x4 d4 = (*(const f32x4*)(dsum + qrow) + *(const f32x4*)(dsum + 64 + qrow)) +
-                         (*(const f32x4*)(dsum + 128 + qrow) + *(const f32x4*)(dsum + 192 + qrow));
+        const f32x4 l4 = *(const f32x4*)(lse_s + qb * 32 + acc_row(4 * x4, h));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { sa[4 * x4 + e] = l4[e]; pa[4 * x4 + e] = -d4[e]; }
+        for (int e = 0; e < 4; ++e) { sa[4 * x4 + e] = l4[e]; pa[4 * x4 + e] = 0.0f; }
     }
 #pragma unroll
     for (int s16 = 0; s16 < D / 16; ++s16) sa = mfma32x32x16(frag_tr(OQ, qb, s16), frag_tr(OK_, kb, s16), sa);
@@ -1462,19 +1433,40 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     for (int s16 = 0; s16 < DV / 16; ++s16) pa = mfma32x32x16(frag_tr(ODO, qb, s16), frag_tr(OV, kb, s16), pa);
     const int kslot = kb * 32 + r;
     const bool kvalid = (kslot & 7) < ws && (kslot >> 3) < ws;
-    // P and dS into [key][query] images, 4 consecutive queries per 8-byte write
+    // P (fp32 for dS, bf16 into the [key][query] image, 4 consecutive queries per 8-byte
+    // write) and this wave's 32-key partial of D = rowsum(P ∘ dP) for each of its queries
+    float pr[16];
 #pragma unroll
     for (int x4 = 0; x4 < 4; ++x4) {
-        typename Frag8<T>::half p4, s4;
+        typename Frag8<T>::half p4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float pr = kvalid ? exp2_fast(sa[4 * x4 + e] * scale_log2) : 0.0f;
-            p4[e] = (T)pr;
-            s4[e] = (T)(pr * pa[4 * x4 + e]);
+            pr[4 * x4 + e] = kvalid ? exp2_fast(sa[4 * x4 + e] * scale_log2) : 0.0f;
+            p4[e] = (T)pr[4 * x4 + e];
         }
-        const int o = kslot * PROW + (qb * 32 + acc_row(4 * x4, h)) * 2;
-        *(typename Frag8<T>::half*)(smem + OP + o) = p4;
-        *(typename Frag8<T>::half*)(smem + ODS + o) = s4;
+        *(typename Frag8<T>::half*)(smem + OP + kslot * PROW + (qb * 32 + acc_row(4 * x4, h)) * 2) = p4;
+    }
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+        float v = pr[x] * pa[x];   // keys on lanes: sum over the 32 lanes of this half (h)
+        v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+        v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+        v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+        v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+        auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+        if (r == 0) dsum[kb * 64 + qb * 32 + acc_row(x, h)] = v;
+    }
+    lds_barrier();
+    // dS = P ∘ (dP − D), D = the two key halves' partials
+#pragma unroll
+    for (int x4 = 0; x4 < 4; ++x4) {
+        const int qrow = qb * 32 + acc_row(4 * x4, h);
+        const f32x4 d4 = *(const f32x4*)(dsum + qrow) + *(const f32x4*)(dsum + 64 + qrow);
+        typename Frag8<T>::half s4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s4[e] = (T)(pr[4 * x4 + e] * (pa[4 * x4 + e] - d4[e]));
+        *(typename Frag8<T>::half*)(smem + ODS + kslot * PROW + qrow * 2) = s4;
     }
     lds_barrier();
     FA_STAMP(3);
