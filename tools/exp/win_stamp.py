@@ -10,7 +10,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "build":
     B = os.path.join(ROOT, "flashattention.jl_amd", "csrc", "build")
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-shared",
                     "-fno-gpu-rdc", f"-DFA_WIN_ABL={ABL}", "-o", SO, "-x", "hip", os.path.join(HERE, "win_stamp.hip"),
-                    "-x", "none", os.path.join(B, "fa_fwd.hip.o"), os.path.join(B, "fa_fwd_p4.hip.o"), os.path.join(B, "fa_bwd.hip.o"),
+                    "-x", "none", os.path.join(B, "fa_fwd.hip.o"), os.path.join(B, "fa_fwd_pers.hip.o"), os.path.join(B, "fa_fwd_p4.hip.o"), os.path.join(B, "fa_bwd.hip.o"),
                     os.path.join(B, "fa_f64.hip.o")], check=True)
     sys.exit(0)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
