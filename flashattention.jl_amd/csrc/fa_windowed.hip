@@ -884,8 +884,11 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
         stage(rq[j], tid + NTH * j, smem, false);
         stage(rk[j], tid + NTH * j, smem + QIMG, false);
     }
-    // LDS-only barrier: the v loads stay in flight across it (a __syncthreads
-    // fence would wait for them) and land under the QK / softmax phase
+    // V staged before the one barrier too (round 5): its loads were issued with Q's and
+    // K's, and staging it after the softmax put a second barrier and the staging on the
+    // path to the stores
+#pragma unroll
+    for (int j = 0; j < NIV; ++j) stage(rv[j], tid + NTH * j, smem + 2 * QIMG, true);
     lds_barrier();
     FA_STAMP(2);
 
@@ -941,10 +944,6 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
         }
     const float lt = swap_halves_sum((ps[0] + ps[1]) + (ps[2] + ps[3]));
     FA_STAMP(4);
-
-#pragma unroll
-    for (int j = 0; j < NIV; ++j) stage(rv[j], tid + NTH * j, smem + 2 * QIMG, true);
-    lds_barrier();
 
     // ---- Oᵀ = Vᵀ·Pᵀ for this wave's 32-feature chunk, stored straight to the pixels ----
     const int qslot = qb * 32 + r, qtx = qslot & 7, qty = qslot >> 3;
