@@ -782,16 +782,29 @@ __device__ __forceinline__ unsigned atomic_add_ret(unsigned* p, unsigned v) {
 template <class X>
 __device__ __forceinline__ void lds_fence(X& x) { asm volatile("" : "+v"(x)); }
 
-// Per-lane variant of shift_row (windows of one workgroup differ in shift).
+// Per-lane variant of shift_row (windows of one workgroup differ in shift; -8 < sh < 8,
+// so the dword shift s2 = floor(sh / 2) is in [-4, 3]): three bit-select levels (1, 2, 4
+// dwords) over the zero-extended row, with lane masks, then the odd pixel by
+// v_alignbyte with the lane's byte shift.  (Written as selects of array elements, the
+// compiler turned the levels into indexed scratch accesses.)
 __device__ __forceinline__ u32x4 shift_row_lane(const u32x4& in, int sh, const unsigned (&mask)[4]) {
-    const int s2 = sh >> 1;
-    const bool odd = (sh & 1) != 0;
-    unsigned e[5];
+    const int u = (sh >> 1) + 4;                     // 0 .. 7: e[j] = ext[j + u] = in[j + s2]
+    const unsigned m1 = 0u - (unsigned)(u & 1), m2 = 0u - (unsigned)((u >> 1) & 1), m4 = 0u - (unsigned)((u >> 2) & 1);
+    auto bfi = [](unsigned m, unsigned x, unsigned y) { return (x & m) | (y & ~m); };
+    unsigned ext[13];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) e[j] = pick_dword(in, j + s2);
+    for (int i = 0; i < 13; ++i) ext[i] = (i >= 4 && i < 8) ? in[i - 4] : 0u;
+    unsigned a1[12], a2[10], e[5];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) a1[i] = bfi(m1, ext[i + 1], ext[i]);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) a2[i] = bfi(m2, a1[i + 2], a1[i]);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) e[j] = bfi(m4, a2[j + 4], a2[j]);
+    const unsigned ab = (sh & 1) ? 2u : 0u;
     u32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = (odd ? __builtin_amdgcn_alignbyte(e[j + 1], e[j], 2u) : e[j]) & mask[j];
+    for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(e[j + 1], e[j], ab) & mask[j];
     return o;
 }
 
@@ -841,8 +854,11 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
     // pair may straddle images); item offsets are relative to image b0
     const int b0 = win_of(0).b;
     const int nimg = min(NWIN == 1 ? 1 : 2, (int)nwin_total / nperimg - b0);
+    // every item of a lane belongs to the same window (NTH is a multiple of NWIN)
+    const int wl_me = NWIN == 1 ? 0 : (int)(tid % NWIN);
+    const Win wme = win_of(wl_me);
     auto item_off = [&](int it, int C) {
-        const Win w = win_of(NWIN == 1 ? 0 : it % NWIN);
+        const Win& w = wme;
         const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3, y = w.y0 + yy;
         const bool ok = w.ok && yy < ws && y >= 0 && y < H_ && f < C;
         if (FA_WIN_ABL & 2) return 0;
@@ -861,34 +877,53 @@ __global__ __launch_bounds__(256 * NWIN) void win_rows1s(const T* __restrict__ q
 #pragma unroll
     for (int j = 0; j < NIV; ++j) rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, item_off(tid + NTH * j, dv), 0, 0);
 
-    // staging of one item: shift into slots, mask (slot < ws, pixel inside the image)
-    auto stage = [&](const u32x4& val, int it, char* img, bool vlayout) {
-        const int wl = NWIN == 1 ? 0 : it % NWIN;
-        const Win w = win_of(wl);
-        const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3;
-        unsigned mask[4];
+    // staging of one item: shift into slots, mask (slot < ws, pixel inside the image).
+    // A lane's window, masks and shift are computed once.  Round 5: when no lane of the wave
+    // shifts by 2 pixels or more (every window away from the image's left and right
+    // edges: ax = xs rounded down to even, so the shift is 0 or 1), the shift is one
+    // v_alignbyte per dword with the lane's byte shift instead of five runtime dword
+    // picks (the staging was ~400 VALU, 163 of them v_cndmask, per lane before the barrier).
+    unsigned mask_me[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int t0 = 2 * j, t1 = 2 * j + 1;
-            const bool v0 = t0 < ws && w.xs + t0 >= 0 && w.xs + t0 < W_;
-            const bool v1 = t1 < ws && w.xs + t1 >= 0 && w.xs + t1 < W_;
-            mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
+    for (int j = 0; j < 4; ++j) {
+        const int t0 = 2 * j, t1 = 2 * j + 1;
+        const bool v0 = t0 < ws && wme.xs + t0 >= 0 && wme.xs + t0 < W_;
+        const bool v1 = t1 < ws && wme.xs + t1 >= 0 && wme.xs + t1 < W_;
+        mask_me[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
+    }
+    const int sh_me = wme.xs - wme.ax;
+    const bool near_shift = NWIN > 1 && __builtin_amdgcn_ballot_w64((sh_me >> 1) != 0) == 0;
+    const unsigned ab_me = (sh_me & 1) ? 2u : 0u;
+    auto stage = [&](auto fast, const u32x4& val, int it, char* img, bool vlayout) {
+        const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3;
+        u32x4 o;
+        if constexpr (NWIN == 1) {
+            o = shift_row(val, sh_me, mask_me);
+        } else if constexpr (decltype(fast)::value) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                o[j] = __builtin_amdgcn_alignbyte(j < 3 ? val[j + 1] : 0u, val[j], ab_me) & mask_me[j];
+        } else {
+            o = shift_row_lane(val, sh_me, mask_me);
         }
-        const u32x4 o = NWIN == 1 ? shift_row(val, w.xs - w.ax, mask) : shift_row_lane(val, w.xs - w.ax, mask);
-        char* base = smem + wl * REGION + (img - smem);
+        char* base = smem + wl_me * REGION + (img - smem);
         const int off = vlayout ? f * VROW + yy * 16 : f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
         *(u32x4*)(base + off) = o;
     };
-#pragma unroll
-    for (int j = 0; j < NIQ; ++j) {
-        stage(rq[j], tid + NTH * j, smem, false);
-        stage(rk[j], tid + NTH * j, smem + QIMG, false);
-    }
     // V staged before the one barrier too (round 5): its loads were issued with Q's and
     // K's, and staging it after the softmax put a second barrier and the staging on the
     // path to the stores
+    auto stage_all = [&](auto fast) {
 #pragma unroll
-    for (int j = 0; j < NIV; ++j) stage(rv[j], tid + NTH * j, smem + 2 * QIMG, true);
+        for (int j = 0; j < NIQ; ++j) {
+            stage(fast, rq[j], tid + NTH * j, smem, false);
+            stage(fast, rk[j], tid + NTH * j, smem + QIMG, false);
+        }
+#pragma unroll
+        for (int j = 0; j < NIV; ++j) stage(fast, rv[j], tid + NTH * j, smem + 2 * QIMG, true);
+    };
+    if (near_shift) stage_all(std::true_type{});
+    else stage_all(std::false_type{});
     lds_barrier();
     FA_STAMP(2);
 
