@@ -714,11 +714,17 @@ __device__ __forceinline__ unsigned pick_dword(const u32x4& in, int idx) {
     return r;
 }
 // out pixel t = in pixel (t + sh) (0 outside 0..7), sh in (-8, 8) wave-uniform,
-// then AND-ed with the per-slot mask.
+// then AND-ed with the per-slot mask.  Interior windows (ax = xs rounded down to even)
+// shift by 0 or 1 pixel: one v_alignbyte per dword (round 5; the runtime dword picks of
+// the general case are kept for windows at the image's left and right edges).
 __device__ __forceinline__ u32x4 shift_row(const u32x4& in, int sh, const unsigned (&mask)[4]) {
     const int s2 = sh >> 1;              // floor(sh / 2)
     u32x4 o;
-    if (sh & 1) {
+    if (s2 == 0) {
+        const unsigned ab = (sh & 1) ? 2u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(j < 3 ? in[j + 1] : 0u, in[j], ab) & mask[j];
+    } else if (sh & 1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             o[j] = __builtin_amdgcn_alignbyte(pick_dword(in, j + s2 + 1), pick_dword(in, j + s2), 2u) & mask[j];
