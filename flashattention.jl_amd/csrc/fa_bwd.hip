@@ -1168,6 +1168,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         uint64_t stall;    // no-progress bound of a poll
         unsigned next_known;   // j + 1's XCD seen (or not needed)
         unsigned pub;      // the last step's publish: kind | ch << 2 | pos << 3 | t << 12
+                           // (pos < K <= CUs < 512; t < 2^20, fused_plan)
         unsigned nodirect; // tests: a chain-B tail never takes the direct add (p.nodirect)
     };
     __shared__ HoffCtx s_hc;
@@ -1725,7 +1726,9 @@ static FusedPlan fused_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
     if (dtype == FA_DTYPE_F32 || dtype == FA_DTYPE_F64 || g_bwd_mode == 1 || g_bwd_force_generic || !shape_fast(dtype, N, Nk, d, dv)) return f;
     const int64_t K = (Nk + 255) / 256, T = (N + 63) / 64;
     const int cus = device_cus(s);
-    if (cus < 8 || g_bwd_hoff * K > T || K > cus || batch * K > INT32_MAX / 2 || 2 * T * (d / 16) * 4096 >= INT32_MAX) return f;
+    if (cus < 8 || g_bwd_hoff * K > T || K > cus || batch * K > INT32_MAX / 2 || 2 * T * (d / 16) * 4096 >= INT32_MAX ||
+        T >= (1 << 20))   // a slice index fits the 20 bits bwd_fused packs it in
+        return f;
     const int xcd = (K <= cus / 8 && batch % 8 == 0 && g_bwd_xcd != 0) ? 1 : 0;
     if (g_bwd_mode == 0) {
         // auto: the grid fills the chip, and K divides the CUs a slab's members are dealt
