@@ -42,6 +42,15 @@
 #define FA_WIN_ABL 0
 #endif
 
+// FA_WIN_PART: this file is compiled twice (Makefile): 1 = the forward entry points (with
+// the scheduler's register-pressure trackers: the strip forward -1.5 % at configs[2]
+// B = 32), 2 = the backward's (without: its strip kernel +0.6 % with them); 0 (a direct
+// include, e.g. the stamp harnesses) = both.  Kernels are templates, so each part emits
+// the ones its entry points instantiate.
+#ifndef FA_WIN_PART
+#define FA_WIN_PART 0
+#endif
+
 namespace fa {
 
 struct WinDev {
@@ -2519,7 +2528,9 @@ static bool rows_f32_ok(const WindowedArgs& a) {
            a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
 }
 
+#if FA_WIN_PART != 2
 thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default for small launches), 10 eight-window strip (the default from kStripMin strips on); modes 7-9 (the rejected LDS-DMA and segment kernels) were removed in round 4
+#endif
 
 // The ONE place the fused-vs-composed decision is made: both the workspace
 // query and the launcher call it, so they can never disagree.
@@ -2664,6 +2675,7 @@ static hipError_t launch_fused(const WindowedArgs& a, const WinDev& g, void* out
 static size_t esize(int dtype) { return dtype_size(dtype); }
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+#if FA_WIN_PART != 2
 size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
     const size_t tok = (size_t)(g.T * g.L * batch);
     if (fused_ok(dtype, g, d, dv))   // direct (no overlap): none; overlap: the window outputs
@@ -2671,7 +2683,9 @@ size_t windowed_fwd_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t
     return align256(tok * d * esize(dtype)) * 2 + align256(tok * dv * esize(dtype)) * 2 +
            align256(dense_fwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) + 256;
 }
+#endif
 
+#if FA_WIN_PART != 2
 size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv, int64_t batch) {
     const size_t tok = (size_t)(g.T * g.L * batch);
     const size_t e = esize(dtype);
@@ -2679,6 +2693,7 @@ size_t windowed_workspace(int dtype, const WindowGeom& g, int64_t d, int64_t dv,
            align256(dense_bwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) +
            align256(dense_fwd_workspace(dtype, g.T, g.T, d, dv, g.L * batch)) + 256;
 }
+#endif
 
 template <class T>
 static hipError_t gather(const void* src, void* dst, int C, int64_t batch, const WinDev& g, bool divide,
@@ -2800,6 +2815,7 @@ static int windowed_fwd_typed(const WindowedArgs& a, hipStream_t s, const char**
     return FA_OK;
 }
 
+#if FA_WIN_PART != 2
 int launch_window(int dtype, const void* src, void* dst, const WindowGeom& geom, int64_t C, int64_t batch,
                   bool unwindow, hipStream_t s, const char** why) {
     if (!geom_fits(geom, C, C, batch) || C > INT32_MAX) {
@@ -2831,7 +2847,9 @@ int launch_window(int dtype, const void* src, void* dst, const WindowGeom& geom,
     }
     return FA_OK;
 }
+#endif
 
+#if FA_WIN_PART != 2
 int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
         *why = "head dimension exceeds the compiled maximum (128)";
@@ -2850,6 +2868,7 @@ int launch_windowed_fwd(const WindowedArgs& a, hipStream_t s, const char** why) 
     *why = "unknown dtype";
     return FA_ERR_INVALID_ARG;
 }
+#endif
 
 template <class T>
 static int windowed_bwd_typed(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
@@ -3033,6 +3052,7 @@ static int windowed_bwd_f32(const WindowedBwdArgs& a, hipStream_t s, const char*
     return FA_OK;
 }
 
+#if FA_WIN_PART != 1
 int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** why) {
     if (a.d > kMaxHeadDim || a.dv > kMaxHeadDim) {
         *why = "head dimension exceeds the compiled maximum (128)";
@@ -3058,5 +3078,6 @@ int launch_windowed_bwd(const WindowedBwdArgs& a, hipStream_t s, const char** wh
     *why = "unknown dtype";
     return FA_ERR_INVALID_ARG;
 }
+#endif
 
 }  // namespace fa

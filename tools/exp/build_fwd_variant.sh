@@ -10,5 +10,5 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-gpu-rdc -munsafe-fp-atomics -
 /opt/rocm/bin/hipcc $F -x hip -c $C/fa_fwd_pers.hip -o $B/fa_fwd_pers.o &
 wait
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $1 $C/build/api.cpp.o $B/fa_fwd.o $B/fa_fwd_pers.o $C/build/fa_fwd_p4.hip.o \
-    $C/build/fa_bwd.hip.o $C/build/fa_windowed.hip.o $C/build/fa_circulant.hip.o $C/build/fa_softmax.hip.o $C/build/fa_f64.hip.o
+    $C/build/fa_bwd.hip.o $C/build/fa_windowed_fwd.o $C/build/fa_windowed_bwd.o $C/build/fa_circulant.hip.o $C/build/fa_softmax.hip.o $C/build/fa_f64.hip.o
 rm -rf $B
