@@ -5,7 +5,7 @@ set -e
 C=/root/repo/flashattention.jl_amd/csrc
 B=/tmp/fwdvar_$$
 mkdir -p $B
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-gpu-rdc -munsafe-fp-atomics -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp $2"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-gpu-rdc -munsafe-fp-atomics -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-use-amdgpu-trackers $2"
 /opt/rocm/bin/hipcc $F -x hip -c $C/fa_fwd.hip -o $B/fa_fwd.o &
 /opt/rocm/bin/hipcc $F -x hip -c $C/fa_fwd_pers.hip -o $B/fa_fwd_pers.o &
 wait
