@@ -38,3 +38,44 @@ def test_checker_sees_a_planted_hazard():
              "\tbuffer_load_dwordx4 v[0:3], v2, s[0:3], 0 offen offset:16 sc1"]
     found = H.scan(lines)
     assert len(found) == 1 and found[0][1].startswith("v_readlane_b32 s87")
+
+
+def test_checker_follows_taken_branches_and_back_edges():
+    import vmem_sgpr_hazards as H
+    # loop head at L0: the back-edge's block ends with a restore 2 wait states before the load
+    loop = ["0000000000001000 <k>:",
+            "\ts_mov_b32 s0, 0",
+            "\ts_nop 7",
+            "",
+            "0000000000001010 <L0>:",
+            "\tbuffer_load_dwordx4 v[0:3], v2, s[0:3], 0 offen sc1",
+            "\ts_nop 7",
+            "\tv_readlane_b32 s2, v9, 3",
+            "\ts_cbranch_scc1 L0",
+            "\ts_endpgm"]
+    found = H.scan(loop)
+    assert len(found) == 1 and found[0][1].startswith("v_readlane_b32 s2") and found[0][3] == 1
+    # an unconditional branch ends its block: the instruction above the label does not fall through
+    jump = ["0000000000001000 <k>:",
+            "\tv_readlane_b32 s2, v9, 3",
+            "\ts_branch L1",
+            "",
+            "0000000000001008 <L0>:",
+            "\tbuffer_load_dwordx4 v[0:3], v2, s[0:3], 0 offen sc1",
+            "",
+            "000000000000100c <L1>:",
+            "\ts_endpgm"]
+    assert not H.scan(jump)
+
+
+def test_disassembly_leaves_the_library_untouched():
+    """objcopy without an output operand rewrites its input in place; a process that has
+    the library mapped then loses its relocated pages (the CPU suite used to segfault in
+    the next C++ unwind after this test)."""
+    import vmem_sgpr_hazards as H
+    if not os.path.exists(LIB) or shutil.which("objcopy") is None:
+        pytest.skip("libfa_hip.so or objcopy missing")
+    before = os.stat(LIB)
+    H.disassemble(LIB)
+    after = os.stat(LIB)
+    assert (before.st_mtime_ns, before.st_ino, before.st_size) == (after.st_mtime_ns, after.st_ino, after.st_size)

@@ -5,8 +5,18 @@ or carry-out) followed, within 5 wait states, by a vector-memory instruction tha
 reads that SGPR as its buffer descriptor or scalar base/offset.  The ISA requires 5
 wait states between the two; the asm buffer loads of fa_bwd.hip carry an `s_nop 4`
 only where a spill restore can land in front of them (the LDS-DMA descriptors), so
-this check guards the others.  Linear scan (the fall-through path; each instruction
-counts one wait state, `s_nop N` counts N + 1).
+this check guards the others.
+
+The walk is branch-aware: backwards from each vector-memory instruction along the
+fall-through path and, at every basic-block label it reaches (llvm-objdump
+`--symbolize-operands`), also into the tail of every block that branches there
+(taken `s_cbranch_*` / `s_branch`, including loop back-edges).  Each instruction
+counts one wait state, `s_nop N` counts N + 1.
+
+The library is only read: the fat binary is extracted with `objcopy --dump-section`
+into a scratch output file.  (Without the output operand objcopy rewrites its input
+in place, which truncates the file under any process that has it mapped: the kernel
+then drops that process's relocated private pages and its next C++ unwind faults.)
 
 Usage: python tools/vmem_sgpr_hazards.py [libfa_hip.so]   (exit 1 if any is found)"""
 import os
@@ -20,6 +30,10 @@ TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)\w+")
 SREG = re.compile(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b")
 VALU_SDST = re.compile(r"^(v_readlane_b32|v_readfirstlane_b32)\s+s(\d+)\b|^v_\w+_e64\s+(?:v\[?\d+(?::\d+\])?,\s*)?s\[(\d+):(\d+)\]")
+HEADER = re.compile(r"^[0-9a-f]+ <(\S+)>:")
+LABEL = re.compile(r"^L\d+$")
+BRANCH = re.compile(r"^(s_cbranch_\w+|s_branch)\s+(L\d+)\b")
+NO_FALLTHROUGH = re.compile(r"^(s_branch|s_endpgm|s_setpc_b64)\b")
 
 
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
@@ -27,11 +41,12 @@ MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 def disassemble(lib):
     """Every translation unit's gfx950 code object (the .hip_fatbin section holds one
-    offload bundle per source file), disassembled."""
+    offload bundle per source file), disassembled with symbolized branch targets."""
     out = []
     with tempfile.TemporaryDirectory() as d:
         fat = os.path.join(d, "fat.bin")
-        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib], check=True)
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib, os.path.join(d, "scratch.so")],
+                       check=True)
         blob = open(fat, "rb").read()
         starts, i = [], blob.find(MAGIC)
         while i >= 0:
@@ -43,8 +58,8 @@ def disassemble(lib):
             open(part, "wb").write(blob[a:z])
             subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
                             f"--targets={TARGET}", f"--output={dev}"], check=True)
-            out += subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", dev], check=True,
-                                  capture_output=True, text=True).stdout.split("\n")
+            out += subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", "--symbolize-operands", dev],
+                                  check=True, capture_output=True, text=True).stdout.split("\n")
     return out
 
 
@@ -58,37 +73,71 @@ def sregs(text):
     return r
 
 
-def scan(lines):
-    found, func = [], "?"
-    ins = []
+def _functions(lines):
+    """[(name, instructions, {instruction index: [labels starting there]})]."""
+    funcs, name, ins, labels = [], None, [], {}
     for line in lines:
-        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        m = HEADER.match(line)
         if m:
-            func, ins = m.group(1), []
+            if LABEL.match(m.group(1)):
+                labels.setdefault(len(ins), []).append(m.group(1))
+                continue
+            if name is not None:
+                funcs.append((name, ins, labels))
+            name, ins, labels = m.group(1), [], {}
             continue
         t = line.strip().split("//")[0].strip()
-        if not t or t.endswith(":"):
-            continue
-        ins.append(t)
-        if not VMEM.match(t):
-            continue
-        ops = t.split(None, 1)[1] if " " in t else ""
-        # SGPR operands of the memory instruction (descriptor, saddr, soffset)
-        srcs = sregs(ops)
-        if not srcs:
-            continue
-        ws = 0
-        for prev in reversed(ins[:-1]):
-            if ws >= 5:
-                break
-            w = VALU_SDST.match(prev)
-            if w:
-                dst = {int(w.group(2))} if w.group(2) else set(range(int(w.group(3)), int(w.group(4)) + 1))
-                if dst & srcs:
-                    found.append((func, prev, t, ws))
-                    break
-            n = re.match(r"^s_nop\s+(?:0x)?([0-9a-f]+)", prev)
-            ws += int(n.group(1), 16 if "0x" in prev else 10) + 1 if n else 1
+        if t and not t.endswith(":"):
+            ins.append(t)
+    if name is not None:
+        funcs.append((name, ins, labels))
+    return funcs
+
+
+def _wait_states(t):
+    n = re.match(r"^s_nop\s+(?:0x)?([0-9a-f]+)", t)
+    return int(n.group(1), 16 if "0x" in t else 10) + 1 if n else 1
+
+
+def scan(lines):
+    found = []
+    for func, ins, labels in _functions(lines):
+        sources = {}  # label -> indices of the branches that target it
+        for i, t in enumerate(ins):
+            b = BRANCH.match(t)
+            if b:
+                sources.setdefault(b.group(2), []).append(i)
+
+        def preds(k):
+            # instructions that can execute right before instruction k
+            out = [s for lab in labels.get(k, []) for s in sources.get(lab, [])]
+            if k - 1 >= 0 and not NO_FALLTHROUGH.match(ins[k - 1]):
+                out.append(k - 1)
+            return out
+
+        for i, t in enumerate(ins):
+            if not VMEM.match(t):
+                continue
+            srcs = sregs(t.split(None, 1)[1] if " " in t else "")
+            if not srcs:
+                continue
+            # depth-first over predecessors: (instruction index, wait states between it and t)
+            stack, seen, hit = [(p, 0) for p in preds(i)], set(), None
+            while stack:
+                j, ws = stack.pop()
+                if ws >= 5 or (j, ws) in seen:
+                    continue
+                seen.add((j, ws))
+                w = VALU_SDST.match(ins[j])
+                if w:
+                    dst = {int(w.group(2))} if w.group(2) else set(range(int(w.group(3)), int(w.group(4)) + 1))
+                    if dst & srcs:
+                        hit = (func, ins[j], t, ws)
+                        break
+                nws = ws + _wait_states(ins[j])
+                stack += [(p, nws) for p in preds(j)]
+            if hit:
+                found.append(hit)
     return found
 
 
