@@ -103,18 +103,17 @@ int fa_max_head_dim(void) { return fa::kMaxHeadDim; }
 // benchmarking: 0 = auto (per head-dim class), 5 / 7 = 8 waves x {1, 2} query
 // blocks per wave on 32x32x16 MFMA; 20 = the default geometries with per-element Q
 // gathers and O stores; 30 = the one-wave-per-SIMD persistent kernel (fa_fwd_p4.hip)
-// where its shape rules allow; 40 = the persistent 8-wave kernel at head dims <= 64
-// (fa_fwd_pers.hip) where its shape rules allow, the default geometries elsewhere.  (The measured-and-rejected 4-wave, 16x16x32 and
-// 4-waves-per-SIMD geometries were removed in round 4; git history keeps them.)
+// where its shape rules allow.  (The measured-and-rejected 4-wave, 16x16x32 and
+// 4-waves-per-SIMD geometries were removed in round 4, the persistent 8-wave d <= 64
+// kernel, a measured tie, in round 6; git history keeps them.)
 int fa_debug_set_fwd_variant(int v) {
     const int old = fa::g_fwd_variant;
-    if (v == 0 || v == 5 || v == 7 || v == 20 || v == 30 || v == 40) fa::g_fwd_variant = v;
+    if (v == 0 || v == 5 || v == 7 || v == 20 || v == 30) fa::g_fwd_variant = v;
     return old;
 }
 
 // Not part of the public header: 30 when the calling thread's last forward ran the
-// one-wave-per-SIMD kernel (fa_fwd_p4.hip), 40 when it ran the persistent 8-wave
-// kernel (fa_fwd_pers.hip), 0 otherwise (tests, bench labels).
+// one-wave-per-SIMD kernel (fa_fwd_p4.hip), 0 otherwise (tests, bench labels).
 int fa_debug_fwd_last_path(void) { return fa::g_fwd_last_path; }
 
 // Not part of the public header: lazy-rescale threshold of the bf16/f16 forward

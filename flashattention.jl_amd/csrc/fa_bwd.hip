@@ -29,8 +29,9 @@
 namespace fa {
 
 // bwd_fused: a poll gives up only when the whole launch has published nothing for this
-// long (fa_debug_set_bwd_stall_us): a safety net, not a scheduling decision (§ bwd_fused)
-constexpr int kStallUs = 100000;
+// long (fa_debug_set_bwd_stall_us): a safety net, not a scheduling decision (§ bwd_fused).
+// The boundary header states the same bound (tests/test_abi.py checks they agree).
+constexpr int kStallUs = FA_BWD_HANDOFF_STALL_US;
 
 // Single-pass hand-off words in the workspace (zeroed per call), in 32-bit words from
 // BwdParams::flags, for `batch` slabs of NS slices and KM members:
@@ -1068,7 +1069,11 @@ __device__ __forceinline__ u32x4 desc_of(const void* base, uint32_t bytes) {
 __device__ __forceinline__ void dma16_asm(const u32x4& desc, uint32_t lds_base, int voff) {
     // s_nop 4: five wait states between a VALU write of the descriptor SGPRs (v_readlane
     // of a spilled SGPR, which the hazard recognizer cannot see past the asm) and the read
+#ifdef FA_BWD_DMA_POL   // experiments: cache policy of the loop's Q / dO DMA (e.g. "nt")
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen " FA_BWD_DMA_POL " lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
+#else
     asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
+#endif
 }
 template <int OFF>
 __device__ __forceinline__ u32x4 load16_sc1_asm(const u32x4& desc, int voff) {
@@ -1922,7 +1927,11 @@ int launch_dense_bwd(const DenseBwdArgs& a, hipStream_t s, const char** why) {
         }
         double* nD = (double*)ws;
         double* nlse = nD + a.N * a.batch;
-        if ((e = hipMemsetD32Async((hipDeviceptr_t)p.hdr, kBwdHdrMagic, 1, s)) != hipSuccess) {   // plan 0
+        // plan 0; word 3 (a chain-B tail left its slice to the combine) belongs to the
+        // current call like word 0, so it is cleared wherever word 0 is written; word 2
+        // (the sticky give-up count) is left alone
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)p.hdr, kBwdHdrMagic, 1, s)) != hipSuccess ||
+            (e = hipMemsetD32Async((hipDeviceptr_t)(p.hdr + 3), 0, 1, s)) != hipSuccess) {
             *why = hipGetErrorString(e);
             return FA_ERR_HIP;
         }

@@ -876,18 +876,9 @@ static SplitPlan split_plan(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t
 // launcher
 // --------------------------------------------------------------------------
 bool launch_dense_fwd_p4(const FwdParams& p, int Dc, int DVc, int dtype, hipStream_t s, hipError_t* err);
-bool launch_dense_fwd_pers(const FwdParams& p, int Dc, int DVc, int dtype, hipStream_t s, hipError_t* err);
 
 template <class T, int D>
 static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t s) {
-    // persistent 8-wave kernel at head dims <= 64 (fa_fwd_pers.hip); variant 40 forces it
-    if (p.fast && D <= 64 && DVc <= 64 && g_fwd_variant == 40) {
-        hipError_t e = hipSuccess;
-        if (launch_dense_fwd_pers(p, D, DVc, std::is_same<T, bf16>::value ? FA_DTYPE_BF16 : FA_DTYPE_F16, s, &e)) {
-            g_fwd_last_path = 40;
-            return e;
-        }
-    }
     // one wave per SIMD, persistent (fa_fwd_p4.hip): the default at d = dv = 128 (5-8 %
     // over the 8-wave kernel, bitwise equal: profiles/r04_fwd_p4_default_d128_ab.log);
     // at 64 the 8-wave kernel stays (p4 is 15 % slower there); variant 30 forces it
@@ -904,8 +895,8 @@ static hipError_t launch_dv(const FwdParams& p, int DVc, dim3 grid, hipStream_t 
         int v = g_fwd_variant;
         // default geometries stage Q / O through LDS when the shape allows (variant 20:
         // the same geometries with per-element Q gathers / O stores, for A/B)
-        const bool wide = p.wide && (v == 0 || v == 5 || v == 7 || v == 30 || v == 40);
-        if (v == 0 || v == 20 || v == 30 || v == 40) v = (D <= 64 && DVc <= 64) ? 7 : 5;
+        const bool wide = p.wide && (v == 0 || v == 5 || v == 7 || v == 30);
+        if (v == 0 || v == 20 || v == 30) v = (D <= 64 && DVc <= 64) ? 7 : 5;
         const int nw = 8;
         const int rows = v == 7 ? 512 : 256;   // query rows per workgroup: w8q2 / w8b64
         FwdParams q = p;

@@ -418,21 +418,41 @@ def backward_handoff_trips(device=None) -> int:
     """Slabs whose single-pass dQ hand-off gave up, counted over EVERY dense_fa_backward
     that has used this stream's scratch buffer (a counter in the workspace header that
     no call resets; it starts at whatever the buffer held, so read it before and after
-    a series of calls and take the difference).  Synchronises the stream."""
+    a series of calls and take the difference).  Synchronises the stream.  Raises
+    FlashAttentionError when the last user of the buffer was not dense_fa_backward, when
+    the header is not a backward header, or when the buffer was reallocated since the
+    first read on this stream (the count would have restarted: a difference across the
+    regrowth would be meaningless)."""
     return _backward_header_word(2, device)
+
+
+_BWD_HDR_MAGIC = 0x46414200   # kBwdHdrMagic (fa_bwd.hip): "FAB\0" | plan in the low byte
+_HDR_PTR = {}                  # (device, stream) -> data_ptr of the scratch buffer at the first header read
 
 
 def _backward_header_word(i: int, device=None) -> int:
     """Word i of the fa_dense_bwd workspace header on this stream's scratch buffer
     (2: the sticky give-up count; 3: the last call left some wrapped slice's A + B to
-    the guarded dQ pass — tests).  Synchronises the stream."""
+    the guarded dQ pass — tests; meaningful only after a single-pass call).
+    Synchronises the stream.  Checks as backward_handoff_trips says."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     stream = torch.cuda.current_stream(device)
-    buf = _WS.get((device.type, device.index, stream.cuda_stream))
+    key = (device.type, device.index, stream.cuda_stream)
+    buf = _WS.get(key)
     _require(buf is not None, "no scratch buffer on this stream yet")
-    off = ((buf.data_ptr() + 255) & ~255) - buf.data_ptr() + 4 * i
+    _require(_WS_LAST.get(key) == "dense_fa_backward",
+             "the last call that used this stream's scratch buffer was not dense_fa_backward")
+    first = _HDR_PTR.setdefault(key, buf.data_ptr())
+    _require(first == buf.data_ptr(),
+             "the scratch buffer was reallocated since the first header read on this stream "
+             "(its sticky counters restarted)")
+    off = ((buf.data_ptr() + 255) & ~255) - buf.data_ptr()
     stream.synchronize()
-    return int(buf[off:off + 4].view(torch.int32).item()) & 0xFFFFFFFF
+    words = [int(w) & 0xFFFFFFFF for w in buf[off:off + 16].view(torch.int32).tolist()]
+    _require((words[0] & 0xFFFFFF00) == _BWD_HDR_MAGIC, "the scratch buffer holds no fa_dense_bwd header")
+    if i == 3:
+        _require((words[0] & 0xFF) == 1, "header word 3 is defined only after a single-pass backward")
+    return words[i]
 
 
 # ----------------------------------------------------------------------------

@@ -34,35 +34,79 @@ end
 
 stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
 
-# Scratch for the C ABI's workspace arguments: ONE buffer per (device, stream), grown on
-# demand and reused, as the Python mirror's _workspace (fa_hip/__init__.py).  Calls on
-# one stream run in order, so reusing the buffer across calls is safe; calls on
-# different streams never share one.  A replaced buffer is freed stream-ordered on the
-# stream that used it.  (Without this cache every backward call allocated its
-# workspace: 268 MB at configs[3], 8.6 GB at configs[4].)
-const _WS = Dict{Tuple{Int,UInt},ROCArray{UInt8,1}}()
+# Scratch for the C ABI's workspace arguments: ONE buffer per device, grown on demand and
+# shared by every call on that device, whatever task or stream makes it (task-local
+# streams come and go with their tasks; a cache keyed by stream would keep one buffer per
+# stream ever seen, each up to the largest workspace a call needed on it).  Use is
+# stream-ordered: every call records an event on its stream after its launches, and a
+# call on another stream first makes its own stream wait on that event (no host
+# synchronisation), so two streams never hold the buffer at once.  Growing synchronises
+# the current stream (which already waits on the previous user) before the old buffer is
+# freed.  Memory: the largest workspace any call on the device needed — e.g. 0.54 GB for
+# configs[3]'s backward (two chains of running dQ sums), 17.2 GB for configs[4]'s
+# 1024 slabs on one GPU.  free_workspaces!() gives it all back.
+const libhip = "libamdhip64"
+hip_check(rc::Cint) = rc == 0 ? nothing : error("HIP runtime error $rc")
+
+mutable struct Scratch
+    buf::ROCArray{UInt8,1}
+    last::UInt                # hipStream_t of the last call that used buf
+    ev::Ptr{Cvoid}            # hipEvent_t recorded on that stream after its launches
+end
+const _WS = Dict{Int,Scratch}()
 const _WS_LOCK = ReentrantLock()
-function workspace(nbytes::Integer)
-    key = (AMDGPU.device_id(AMDGPU.device()), UInt(stream_ptr()))
+
+# f(ws) with this device's scratch buffer of at least nbytes; f enqueues on stream_ptr()
+function with_workspace(f, nbytes::Integer)
+    n = max(Int(nbytes), 1)
+    dev = AMDGPU.device_id(AMDGPU.device())
+    s = stream_ptr()
     lock(_WS_LOCK) do
-        buf = get(_WS, key, nothing)
-        if buf === nothing || length(buf) < max(Int(nbytes), 1)
-            buf === nothing || AMDGPU.unsafe_free!(buf)
-            buf = ROCArray{UInt8}(undef, max(Int(nbytes), 1))
-            _WS[key] = buf
+        e = get(_WS, dev, nothing)
+        if e === nothing
+            ev = Ref{Ptr{Cvoid}}(C_NULL)
+            hip_check(ccall((:hipEventCreateWithFlags, libhip), Cint, (Ref{Ptr{Cvoid}}, Cuint), ev, 0x2))  # DisableTiming
+            e = Scratch(ROCArray{UInt8}(undef, n), UInt(s), ev[])
+            _WS[dev] = e
+        elseif e.last != UInt(s)
+            # the event was recorded on the previous user's stream after its launches
+            hip_check(ccall((:hipStreamWaitEvent, libhip), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cuint), s, e.ev, 0))
+            e.last = UInt(s)
         end
-        buf
+        if length(e.buf) < n
+            hip_check(ccall((:hipStreamSynchronize, libhip), Cint, (Ptr{Cvoid},), s))
+            AMDGPU.unsafe_free!(e.buf)
+            e.buf = ROCArray{UInt8}(undef, n)
+        end
+        r = f(e.buf)
+        hip_check(ccall((:hipEventRecord, libhip), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), e.ev, s))
+        r
     end
 end
 
-# dense_fa!(O, l, m, Q, K, V) — replaces the body of src/dense.jl:21-102
-function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
-                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T}
+# Frees every cached scratch buffer (after the work that used them has finished).
+function free_workspaces!()
+    lock(_WS_LOCK) do
+        for (_, e) in _WS
+            hip_check(ccall((:hipEventSynchronize, libhip), Cint, (Ptr{Cvoid},), e.ev))
+            AMDGPU.unsafe_free!(e.buf)
+            hip_check(ccall((:hipEventDestroy, libhip), Cint, (Ptr{Cvoid},), e.ev))
+        end
+        empty!(_WS)
+    end
+    nothing
+end
+
+# dense_fa!(O, l, m, Q, K, V) — replaces the body of src/dense.jl:21-102, with the
+# kernels' own statistics type (Float32 l, m)
+function dense_fa_f32!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T}
     N, d, B = size(Q)
     Nk, dv = size(K, 1), size(V, 2)
     size(K) == (Nk, d, B) || throw(DimensionMismatch("K"))
     size(V) == (Nk, dv, B) || throw(DimensionMismatch("V"))
     size(O) == (N, dv, B) || throw(DimensionMismatch("O"))
+    size(l) == (N, 1, B) && size(m) == (N, 1, B) || throw(DimensionMismatch("l, m must be (N, 1, batch)"))
     nws = ccall((:fa_dense_fwd_workspace, libfa_hip), Csize_t,
                 (Cint, Int64, Int64, Int64, Int64, Int64), fa_dtype(T), N, Nk, d, dv, B)
     if nws == 0
@@ -71,28 +115,55 @@ function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32
                         Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
                        fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, stream_ptr()))
     else   # ragged Nk: zero-padded K / V copies in the workspace let the fast kernels run
-        ws = workspace(nws)
-        fa_check(ccall((:fa_dense_fwd_ws, libfa_hip), Cint,
-                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
-                        Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
-                       fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, ws, nws, stream_ptr()))
+        with_workspace(nws) do ws
+            fa_check(ccall((:fa_dense_fwd_ws, libfa_hip), Cint,
+                           (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                            Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                           fa_dtype(T), Q, K, V, O, l, m, N, Nk, d, dv, B, 0f0, ws, nws, stream_ptr()))
+        end
     end
     return O, l, m
 end
 
-# l, m in any other element type — what the reference's own wrapper allocates,
+# l, m in another element type — what the reference's own wrapper allocates,
 # `l = similar(Q, N, 1, B)` (src/dense.jl:12-13), i.e. T itself for Float64, Float16 and
 # BFloat16 inputs.  The C ABI writes float32 statistics: they are staged in Float32 and
 # converted on the device (for Float64 the kernels keep l, m in double internally and
 # round them to Float32 at this boundary, DESIGN.md §3).
-function dense_fa!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
-                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T,S}
+function dense_fa_staged!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
+                          Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T,S}
     size(l) == size(m) || throw(DimensionMismatch("l, m"))
     lf, mf = similar(l, Float32), similar(m, Float32)
-    dense_fa!(O, lf, mf, Q, K, V)
+    dense_fa_f32!(O, lf, mf, Q, K, V)
     l .= lf
     m .= mf
     return O, l, m
+end
+
+# Methods on the reference's generic function.  Dispatch by construction: for every call
+# the methods that apply include one that is a subtype of all the others, the
+# reference's `dense_fa!(O::AbstractArray{T,3}, l::AbstractArray{T,3}, …) where {T}`
+# (src/dense.jl:21-27) included, so no call is ambiguous
+# (tests/test_julia_binding.py::test_dispatch_has_a_most_specific_hip_method).
+#   T data, Float32 statistics (the C ABI's types)
+function dense_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T}
+    return dense_fa_f32!(O, l, m, Q, K, V)
+end
+#   everything of one type T: a strict subtype of the reference's method
+function dense_fa!(O::ROCArray{T,3}, l::ROCArray{T,3}, m::ROCArray{T,3},
+                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T}
+    return dense_fa_staged!(O, l, m, Q, K, V)
+end
+#   everything Float32: the three methods above and the reference's all apply
+function dense_fa!(O::ROCArray{Float32,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                   Q::ROCArray{Float32,3}, K::ROCArray{Float32,3}, V::ROCArray{Float32,3})
+    return dense_fa_f32!(O, l, m, Q, K, V)
+end
+#   any other statistics type S
+function dense_fa!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
+                   Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}) where {T,S}
+    return dense_fa_staged!(O, l, m, Q, K, V)
 end
 
 # dense_fa(q, k, v) — src/dense.jl:1-19 (l, m are Float32 on the device: DESIGN.md)
@@ -111,10 +182,10 @@ end
 # `handoff`: optional Ref{Cint} that receives fa_dense_bwd_handoff_status after the call
 # (-1 two-pass form, 0 single pass completed, 1 a slab's dQ hand-off gave up and its dQ was
 # recomputed); it synchronises the stream.
-function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
-                           O::ROCArray{T,3}, dO::ROCArray{T,3},
-                           l::ROCArray{Float32,3}, m::ROCArray{Float32,3};
-                           handoff::Union{Nothing,Base.RefValue{Cint}}=nothing) where {T}
+function dense_fa_backward_f32(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
+                               O::ROCArray{T,3}, dO::ROCArray{T,3},
+                               l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                               handoff::Union{Nothing,Base.RefValue{Cint}}) where {T}
     N, d, B = size(Q)
     Nk, dv = size(K, 1), size(V, 2)
     size(K) == (Nk, d, B) && size(V) == (Nk, dv, B) ||
@@ -126,26 +197,47 @@ function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
     dQ, dK, dV = similar(Q), similar(K), similar(V)
     nws = ccall((:fa_dense_bwd_workspace, libfa_hip), Csize_t,
                 (Cint, Int64, Int64, Int64, Int64, Int64), fa_dtype(T), N, Nk, d, dv, B)
-    ws = workspace(nws)
-    fa_check(ccall((:fa_dense_bwd, libfa_hip), Cint,
-                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32},
-                    Ptr{Float32}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
-                    Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
-                   fa_dtype(T), Q, K, V, O, dO, l, m, dQ, dK, dV, N, Nk, d, dv, B, 0f0,
-                   ws, nws, stream_ptr()))
-    if handoff !== nothing
-        fa_check(ccall((:fa_dense_bwd_handoff_status, libfa_hip), Cint,
-                       (Ptr{Cvoid}, Csize_t, Ptr{Cvoid}, Ptr{Cint}), ws, nws, stream_ptr(), handoff))
+    with_workspace(nws) do ws
+        fa_check(ccall((:fa_dense_bwd, libfa_hip), Cint,
+                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32},
+                        Ptr{Float32}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
+                        Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                       fa_dtype(T), Q, K, V, O, dO, l, m, dQ, dK, dV, N, Nk, d, dv, B, 0f0,
+                       ws, nws, stream_ptr()))
+        if handoff !== nothing
+            fa_check(ccall((:fa_dense_bwd_handoff_status, libfa_hip), Cint,
+                           (Ptr{Cvoid}, Csize_t, Ptr{Cvoid}, Ptr{Cint}), ws, nws, stream_ptr(), handoff))
+        end
     end
     return dQ, dK, dV
 end
 
-# the backward with l, m in the caller's element type (from the dense_fa! method above)
+# Methods on the reference's generic function (src/dense.jl:104-111, `… l, m ::
+# AbstractArray{T,3}) where T`), laid out as dense_fa!'s: T data with Float32 statistics,
+# one type T throughout, all Float32, any other statistics type S.
+function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
+                           O::ROCArray{T,3}, dO::ROCArray{T,3},
+                           l::ROCArray{Float32,3}, m::ROCArray{Float32,3};
+                           handoff::Union{Nothing,Base.RefValue{Cint}}=nothing) where {T}
+    return dense_fa_backward_f32(Q, K, V, O, dO, l, m, handoff)
+end
+function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
+                           O::ROCArray{T,3}, dO::ROCArray{T,3},
+                           l::ROCArray{T,3}, m::ROCArray{T,3};
+                           handoff::Union{Nothing,Base.RefValue{Cint}}=nothing) where {T}
+    return dense_fa_backward_f32(Q, K, V, O, dO, Float32.(l), Float32.(m), handoff)
+end
+function dense_fa_backward(Q::ROCArray{Float32,3}, K::ROCArray{Float32,3}, V::ROCArray{Float32,3},
+                           O::ROCArray{Float32,3}, dO::ROCArray{Float32,3},
+                           l::ROCArray{Float32,3}, m::ROCArray{Float32,3};
+                           handoff::Union{Nothing,Base.RefValue{Cint}}=nothing)
+    return dense_fa_backward_f32(Q, K, V, O, dO, l, m, handoff)
+end
 function dense_fa_backward(Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3},
                            O::ROCArray{T,3}, dO::ROCArray{T,3},
                            l::ROCArray{S,3}, m::ROCArray{S,3};
                            handoff::Union{Nothing,Base.RefValue{Cint}}=nothing) where {T,S}
-    return dense_fa_backward(Q, K, V, O, dO, Float32.(l), Float32.(m); handoff=handoff)
+    return dense_fa_backward_f32(Q, K, V, O, dO, Float32.(l), Float32.(m), handoff)
 end
 
 # windowed_fa(q, k, v, ws; stride, pad) — src/windowed.jl:3-23 (fused on the device)
@@ -161,13 +253,14 @@ function windowed_fa(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,N}, windo
     nws = ccall((:fa_windowed_fwd_workspace, libfa_hip), Csize_t,
                 (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),
                 fa_dtype(T), nsp, spatial, d, dv, B, windowsize, stride, pad)
-    ws = workspace(nws)
-    fa_check(ccall((:fa_windowed_fwd, libfa_hip), Cint,
-                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
-                    Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64, Cfloat,
-                    Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
-                   fa_dtype(T), q, k, v, y, l, m, nsp, spatial, d, dv, B, windowsize, stride, pad,
-                   0f0, ws, nws, stream_ptr()))
+    with_workspace(nws) do ws
+        fa_check(ccall((:fa_windowed_fwd, libfa_hip), Cint,
+                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                        Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64, Cfloat,
+                        Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                       fa_dtype(T), q, k, v, y, l, m, nsp, spatial, d, dv, B, windowsize, stride, pad,
+                       0f0, ws, nws, stream_ptr()))
+    end
     return y, l, m
 end
 
@@ -192,13 +285,14 @@ function windowed_fa_backward(q::ROCArray{T,N}, k::ROCArray{T,N}, v::ROCArray{T,
     nws = ccall((:fa_windowed_workspace, libfa_hip), Csize_t,
                 (Cint, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64),
                 fa_dtype(T), nsp, spatial, d, dv, B, windowsize, stride, pad)
-    ws = workspace(nws)
-    fa_check(ccall((:fa_windowed_bwd, libfa_hip), Cint,
-                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
-                    Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64,
-                    Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
-                   fa_dtype(T), q, k, v, y, dy, l, m, dq, dk, dv_, nsp, spatial, d, dv, B,
-                   windowsize, stride, pad, 0f0, ws, nws, stream_ptr()))
+    with_workspace(nws) do ws
+        fa_check(ccall((:fa_windowed_bwd, libfa_hip), Cint,
+                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
+                        Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Int64}, Int64, Int64, Int64, Int64, Int64, Int64,
+                        Cfloat, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                       fa_dtype(T), q, k, v, y, dy, l, m, dq, dk, dv_, nsp, spatial, d, dv, B,
+                       windowsize, stride, pad, 0f0, ws, nws, stream_ptr()))
+    end
     return dq, dk, dv_
 end
 
@@ -235,13 +329,14 @@ block_fa(q::ROCArray, k::ROCArray, v::ROCArray, windowsize; pad=0) =
     windowed_fa(q, k, v, windowsize; stride=windowsize, pad=pad)
 
 # circulant_fa!(O, l, m, Q, K, V, W) — replaces src/circulant.jl:9-118
-function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
-                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
+function circulant_fa_f32!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                           Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
     N, d, B = size(Q)
     dv = size(V, 2)
     size(K) == (N, d, B) || throw(DimensionMismatch("K"))
     size(V) == (N, dv, B) || throw(DimensionMismatch("V"))
     size(O) == (N, dv, B) || throw(DimensionMismatch("O"))
+    size(l) == (N, 1, B) && size(m) == (N, 1, B) || throw(DimensionMismatch("l, m must be (N, 1, batch)"))
     fa_check(ccall((:fa_circulant_fwd, libfa_hip), Cint,
                    (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32},
                     Int64, Int64, Int64, Int64, Int64, Cfloat, Ptr{Cvoid}),
@@ -249,15 +344,34 @@ function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Flo
     return O, l, m
 end
 
-# circulant_fa! with l, m in the caller's element type (staged in Float32, as dense_fa!)
-function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
-                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T,S}
+# l, m in another element type, staged in Float32 as dense_fa_staged! does
+function circulant_fa_staged!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
+                              Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T,S}
     size(l) == size(m) || throw(DimensionMismatch("l, m"))
     lf, mf = similar(l, Float32), similar(m, Float32)
-    circulant_fa!(O, lf, mf, Q, K, V, W)
+    circulant_fa_f32!(O, lf, mf, Q, K, V, W)
     l .= lf
     m .= mf
     return O, l, m
+end
+
+# Methods on the reference's generic function (src/circulant.jl:9-16, `… ::AbstractArray{T,3},
+# W::Int) where {T}`), laid out as dense_fa!'s.
+function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
+    return circulant_fa_f32!(O, l, m, Q, K, V, W)
+end
+function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{T,3}, m::ROCArray{T,3},
+                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T}
+    return circulant_fa_staged!(O, l, m, Q, K, V, W)
+end
+function circulant_fa!(O::ROCArray{Float32,3}, l::ROCArray{Float32,3}, m::ROCArray{Float32,3},
+                       Q::ROCArray{Float32,3}, K::ROCArray{Float32,3}, V::ROCArray{Float32,3}, W::Int)
+    return circulant_fa_f32!(O, l, m, Q, K, V, W)
+end
+function circulant_fa!(O::ROCArray{T,3}, l::ROCArray{S,3}, m::ROCArray{S,3},
+                       Q::ROCArray{T,3}, K::ROCArray{T,3}, V::ROCArray{T,3}, W::Int) where {T,S}
+    return circulant_fa_staged!(O, l, m, Q, K, V, W)
 end
 
 # circulant_fa(Q, K, V, W) — src/circulant.jl:1-7, passing W (the reference call drops it)
@@ -276,10 +390,11 @@ function fused_softmax!(P::ROCArray{T,3}, S::ROCArray{T,3}; dims=1) where {T}
     size(P) == size(S) || throw(DimensionMismatch("P and S must have the same size"))
     M, N, B = size(S)
     nws = ccall((:fa_softmax_workspace, libfa_hip), Csize_t, (Int64, Int64, Int64, Cint), M, N, B, dims)
-    ws = workspace(nws)
-    fa_check(ccall((:fa_softmax, libfa_hip), Cint,
-                   (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Int64, Cint, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
-                   fa_dtype(T), S, P, M, N, B, dims, ws, nws, stream_ptr()))
+    with_workspace(nws) do ws
+        fa_check(ccall((:fa_softmax, libfa_hip), Cint,
+                       (Cint, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Int64, Cint, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                       fa_dtype(T), S, P, M, N, B, dims, ws, nws, stream_ptr()))
+    end
     return P
 end
 fused_softmax!(P::ROCArray{T,2}, S::ROCArray{T,2}; dims=1) where {T} =

@@ -99,8 +99,9 @@ size_t fa_dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
  * a 256-B header (fa_dense_bwd_handoff_status), 8·N·batch bytes of row
  * statistics; for bf16 / fp16 shapes outside the MFMA kernels' set, zero-padded
  * copies; and when the single-pass kernel applies (grids that
- * fill the chip), per-slice counters plus the running fp32 dQ sums,
- * 4·N·d·batch bytes (8.6 GB for configs[4]'s 1024 slabs of (16384, 128)).  A
+ * fill the chip), per-slice counters plus the running fp32 dQ sums of the two
+ * chains per slice, 2·4·N·d·batch bytes (17.2 GB for configs[4]'s 1024 slabs of
+ * (16384, 128)).  A
  * smaller workspace that still holds the first parts (the size this function
  * returns under fa_debug_set_bwd_mode(1)) runs the two-pass form instead.  The
  * answer depends on the current device's CU count. */
@@ -115,12 +116,16 @@ size_t fa_dense_bwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d,
  * l, m are the forward's outputs.  dQ, dK, dV are fully written, without
  * atomics.  dK and dV are bitwise reproducible.  dQ is bitwise reproducible
  * whenever the single pass's ordered dQ hand-off completes (it sums each query
- * slice over the key blocks in a fixed order).  If a slab's hand-off gives up —
- * its members could not all be resident (other streams or processes holding CUs:
- * a wait sees no new member arrive within 50 us) or a wait passes 20 ms — dQ of
- * that slab is recomputed by a separate pass that sums in a different order: same
- * values within rounding, not the same bits, and slower.
- * fa_dense_bwd_handoff_status reports whether any slab did. */
+ * slice over the key blocks in a fixed order).  Every hand-off wait is on a
+ * workgroup dispatched earlier in the same launch, so no co-residency is needed:
+ * other streams or processes sharing the GPU slow the call down but do not make it
+ * give up.  A wait gives up only as a safety net, when neither the launch's arrival
+ * count nor any member of the waiting slab has made progress for
+ * FA_BWD_HANDOFF_STALL_US microseconds (100 ms); dQ of that slab is then recomputed
+ * by a separate pass that sums in a different order: same values within rounding,
+ * not the same bits, and slower.  fa_dense_bwd_handoff_status reports whether any
+ * slab did. */
+#define FA_BWD_HANDOFF_STALL_US 100000
 int fa_dense_bwd(int dtype,
                  const void* Q, const void* K, const void* V,
                  const void* O, const void* dO,

@@ -32,6 +32,24 @@ def test_header_declares_the_boundary():
         assert f in fns
 
 
+def test_header_states_the_kernels_give_up_bound():
+    """The boundary contract's hand-off give-up bound is the one bwd_fused implements:
+    fa_bwd.hip takes kStallUs from the header's macro, and the prose around it states
+    the same figure (in ms) and the no-progress rule (INTEGRATION.md agrees)."""
+    hdr = open(HEADER).read()
+    m = re.search(r"#define\s+FA_BWD_HANDOFF_STALL_US\s+(\d+)", hdr)
+    assert m, "FA_BWD_HANDOFF_STALL_US missing from fa_hip.h"
+    us = int(m.group(1))
+    src = open(os.path.join(ROOT, "flashattention.jl_amd", "csrc", "fa_bwd.hip")).read()
+    k = re.search(r"constexpr\s+int\s+kStallUs\s*=\s*(\w+)\s*;", src)
+    assert k and k.group(1) in ("FA_BWD_HANDOFF_STALL_US", str(us)), "kStallUs does not follow the header"
+    prose = re.sub(r"\s+", " ", hdr)
+    assert f"({us // 1000} ms)" in prose and "made progress" in prose
+    assert "50 us" not in prose and "20 ms" not in prose
+    integ = re.sub(r"\s+", " ", open(os.path.join(ROOT, "INTEGRATION.md")).read())
+    assert f"{us // 1000} ms" in integ
+
+
 def test_library_loads_and_exports_every_declared_symbol():
     import fa_hip
     L = fa_hip.lib()

@@ -31,6 +31,9 @@ for p in paths:
     # AB_L2LOCAL=0/1: force the single pass's L2-local hand-off form in every build
     if os.environ.get("AB_L2LOCAL") is not None and hasattr(libs[-1], "fa_debug_set_bwd_l2local"):
         libs[-1].fa_debug_set_bwd_l2local(int(os.environ["AB_L2LOCAL"]))
+    # AB_HOFF=k: the single pass's chain step offset in every build
+    if os.environ.get("AB_HOFF") is not None:
+        libs[-1].fa_debug_set_bwd_hoff(int(os.environ["AB_HOFF"]))
 rounds = int(os.environ.get("AB_ROUNDS", 6))
 for (N, d, BH) in shapes:
     g = torch.Generator(device="cuda").manual_seed(1)

@@ -1,9 +1,11 @@
 """Run a workload back-to-back for a few seconds while sampling the GPU's clock
 and power with rocm-smi in child processes: tells whether a kernel is
-power/clock-capped (DVFS) or issue-bound at full clock.
-Usage: python tools/exp/clock_probe.py [seconds] [fwd|fwd128|gemm|bwd]..."""
+power/clock-capped (DVFS) or issue-bound at full clock.  Prints TFLOP/s, the mean
+of the power and sclk samples, and the energy per FLOP (pJ/FLOP = W / FLOP/s) so
+kernels can be compared at the board's power cap.
+Usage: python tools/power_probe.py [seconds] [fwd|fwd128|gemm|bwd]..."""
 import os, subprocess, sys, time
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "flashattention.jl_amd")]
 import torch
 import fa_hip
@@ -43,9 +45,14 @@ def smi():
 
 
 def parse(txt):
+    """(watts, MHz) of one rocm-smi sample (None where absent)."""
     pw = [l.split(":")[-1].strip() for l in txt.splitlines() if "Power (W)" in l]
-    sc = [l.split("(")[-1].rstrip(")") for l in txt.splitlines() if "sclk" in l]
-    return f"power {pw[0] if pw else '?'} W, sclk {sc[0] if sc else '?'}"
+    sc = [l.split("(")[-1].rstrip(")").lower().replace("mhz", "") for l in txt.splitlines() if "sclk" in l]
+    f = lambda v: float(v[0]) if v else None
+    try:
+        return f(pw), f(sc)
+    except ValueError:
+        return None, None
 
 
 for mode in modes:
@@ -66,8 +73,14 @@ for mode in modes:
             next_probe += secs / 5
     e1.record(); torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / n
-    readings = "; ".join(parse(p.communicate(timeout=60)[0]) for p in probes)
-    print(f"{mode}: {n} launches, {t*1e6:.1f} us each, {flops/t/1e12:.1f} TFLOP/s | {readings}", flush=True)
+    samples = [parse(p.communicate(timeout=60)[0]) for p in probes]
+    w = [a for a, _ in samples if a is not None]
+    mhz = [b for _, b in samples if b is not None]
+    tf = flops / t / 1e12
+    wm = sum(w) / len(w) if w else float("nan")
+    mm = sum(mhz) / len(mhz) if mhz else float("nan")
+    print(f"{mode}: {n} launches, {t*1e6:.1f} us each, {tf:.1f} TFLOP/s | power {wm:.0f} W, sclk {mm:.0f} MHz, "
+          f"{wm / (tf * 1e12) * 1e12:.3f} pJ/FLOP | samples {samples}", flush=True)
     del fn
     torch.cuda.empty_cache()
     time.sleep(2)
