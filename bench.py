@@ -293,12 +293,31 @@ def _mfma_roofline(flops, seconds, kernel, note=None):
     return r
 
 
-def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
+def _traffic_json(kind: str, workload: str):
+    """The newest committed PMC summary profiles/*<kind>_traffic*.json for `workload`
+    (written from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes with the gfx950
+    FETCH_SIZE x2 correction), or None."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{kind}_traffic*.json"))):
+        try:
+            j = json.load(open(p))
+        except Exception:
+            continue
+        if j.get("workload", "").startswith(workload):
+            best = j
+    return best
+
+
+def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5, settle_s=0.25):
     """BASELINE configs[3]: dense_fa bf16 (B,H,N,d) = (4,16,8192,128) forward,
     backward (reference src/dense.jl:104-167, executable spec
     src_cpp/FlashAttention.cpp:194-252) and forward+backward.  FLOPs: forward
     4·BH·N²·d, backward 2.5x, fwd+bwd 3.5x.  Device time by
-    HIP events on the launch stream; ~60 ms of GPU time."""
+    HIP events on the launch stream.  Each leg is timed twice: `*_cold` right
+    after its warm-up calls, then again after `settle_s` of untimed back-to-back
+    calls of the same leg (the configs[1] line's disclosed settle, DESIGN.md §6);
+    the headline fields are the settled ones."""
     gen = torch.Generator(device="cuda").manual_seed(7)
     N, d, BH = 8192, 128, 64
     Q, K, V, dO = (_randn_jl(fa, (N, d, BH), torch.bfloat16, gen) for _ in range(4))
@@ -306,30 +325,45 @@ def cfg3_block(fa, dist, steps_fwd=10, steps_bwd=5):
     l = fa.jl_empty((N, 1, BH))
     m = fa.jl_empty((N, 1, BH))
     f = 4.0 * BH * N * N * d
-    _, e_f = time_region(lambda: fa.dense_fa_(O, l, m, Q, K, V), steps_fwd, 2, dist)
-    t_f = e_f / steps_fwd
+    fwd = lambda: fa.dense_fa_(O, l, m, Q, K, V)
+    _, e_fc = time_region(fwd, steps_fwd, 2, dist)
+    n_sf, s_sf = settle(fwd, settle_s)
+    _, e_f = time_region(fwd, steps_fwd, 0, dist)
+    t_f, t_fc = e_f / steps_fwd, e_fc / steps_fwd
     k_f = _fwd_kernel_128(fa)
     fa.dense_fa_backward(Q, K, V, O, dO, l, m)   # the stream's scratch buffer exists before the count is read
     trips0 = fa.backward_handoff_trips(Q.device)
-    _, e_b = time_region(lambda: fa.dense_fa_backward(Q, K, V, O, dO, l, m), steps_bwd, 1, dist)
-    t_b = e_b / steps_bwd
+    bwd = lambda: fa.dense_fa_backward(Q, K, V, O, dO, l, m)
+    _, e_bc = time_region(bwd, steps_bwd, 1, dist)
+    n_sb, s_sb = settle(bwd, settle_s)
+    _, e_b = time_region(bwd, steps_bwd, 0, dist)
+    t_b, t_bc = e_b / steps_bwd, e_bc / steps_bwd
     hs = fa.backward_handoff_status(Q.device)   # the last timed call
-    # slabs that gave up over the warm-up and timed calls: a counter in the workspace
-    # header that no call resets (fa_hip.backward_handoff_trips), read around them
+    # slabs that gave up over the warm-up, settle and timed calls: a counter in the
+    # workspace header that no call resets (fa_hip.backward_handoff_trips), read around them
     trips = (fa.backward_handoff_trips(Q.device) - trips0) & 0xFFFFFFFF
+    rb = _mfma_roofline(
+        2.5 * f, t_b, "fa::bwd_fused<bf16,128,128>",
+        "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + bwd_fused + the guarded dQ pass), "
+        "FLOPs = 2.5x forward (the 5 GEMMs of the single pass)")
+    tj = _traffic_json("bwd", "configs[3]")
+    rb["traffic"] = tj.get("hbm_bytes_per_launch") if tj else None
+    if tj:
+        rb["traffic_over_algorithmic"] = tj.get("ratio_to_algorithmic")
+        rb["traffic_source"] = "profiles/r06_bwd_traffic.json (rocprofv3 PMC, bwd_fused per launch)"
     res = {
         "workload": "configs[3]: dense_fa bf16 forward + backward, (B,H,N,d)=(4,16,8192,128)",
         "fwd_tflops": f / t_f / 1e12, "bwd_tflops": 2.5 * f / t_b / 1e12,
         "fwd_bwd_tflops": 3.5 * f / (t_f + t_b) / 1e12,
         "fwd_ms": t_f * 1e3, "bwd_ms": t_b * 1e3, "steps_fwd": steps_fwd, "steps_bwd": steps_bwd,
+        "fwd_tflops_cold": f / t_fc / 1e12, "bwd_tflops_cold": 2.5 * f / t_bc / 1e12,
+        "fwd_ms_cold": t_fc * 1e3, "bwd_ms_cold": t_bc * 1e3,
+        "settle": {"fwd_launches": n_sf, "fwd_ms": s_sf * 1e3, "bwd_launches": n_sb, "bwd_ms": s_sb * 1e3},
         "roofline_fwd": _mfma_roofline(f, t_f, k_f),
-        "roofline_bwd": _mfma_roofline(
-            2.5 * f, t_b, "fa::bwd_fused<bf16,128,128>",
-            "whole fa_dense_bwd call (D = rowsum(dO*O) pre-pass + bwd_fused + the guarded dQ pass), "
-            "FLOPs = 2.5x forward (the 5 GEMMs of the single pass)"),
+        "roofline_bwd": rb,
         "roofline_fwd_bwd": _mfma_roofline(3.5 * f, t_f + t_b, "forward + backward calls"),
         "bwd_handoff": {-1: "two-pass plan (no hand-off)", 0: "single pass, hand-off completed",
-                        1: "single pass, a slab's hand-off GAVE UP (members not co-resident): its dQ recomputed by the guarded pass"}.get(hs, hs),
+                        1: "single pass, a slab's hand-off GAVE UP (the launch made no progress for 100 ms): its dQ recomputed by the guarded pass"}.get(hs, hs),
         "bwd_handoff_giveups": trips,
         "bwd_fallback_tainted": trips != 0 or hs == 1,
     }
@@ -508,20 +542,11 @@ def cpu_baseline(node: bool = False):
 
 
 def _traffic_from_profiles():
-    """HBM bytes per launch of the forward kernel from the committed rocprofv3
-    PMC summary (profiles/*fwd_traffic*.json, written by
-    profiles/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes with
-    the gfx950 FETCH_SIZE x2 correction), newest for this workload."""
-    import glob
-    best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*fwd_traffic*.json"))):
-        try:
-            j = json.load(open(p))
-        except Exception:
-            continue
-        if j.get("workload") == "configs[1]":
-            best = j.get("hbm_bytes_per_launch")
-    return best
+    """HBM bytes per launch of the configs[1] forward kernel from the committed
+    rocprofv3 PMC summary (profiles/*fwd_traffic*.json, written by
+    profiles/pmc_traffic.py)."""
+    j = _traffic_json("fwd", "configs[1]")
+    return j.get("hbm_bytes_per_launch") if j else None
 
 
 def _free_port():
@@ -561,6 +586,8 @@ def main():
                     help="cpu_baseline also on every affinity CPU (beyond the box's per-GPU share)")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the configs[4] strong-scaling block")
     ap.add_argument("--no-cfg23", action="store_true", help="skip the configs[2] / configs[3] blocks")
+    ap.add_argument("--no-cfg2", action="store_true", help="skip the configs[2] block")
+    ap.add_argument("--no-cfg3", action="store_true", help="skip the configs[3] block")
     ap.add_argument("--extra", action="store_true", help="also time the secondary paths (reported under 'extra')")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -640,12 +667,13 @@ def main():
     if cpu_hook:
         out["cpu_step_hook"] = True
 
-    if not args.no_cfg23 and not cpu_hook:
-        out["cfg3"] = cfg3_block(fa_hip, dist)
+    if not (args.no_cfg23 or args.no_cfg3) and not cpu_hook:
+        out["cfg3"] = cfg3_block(fa_hip, dist, settle_s=args.settle_ms / 1e3)
         if shared_gpu:
             # co-tenant ranks: the single pass needs no co-residency (every hand-off wait
             # is on an earlier-dispatched workgroup), so it stays the plan here too
             out["cfg3"]["bwd_plan"] = "single pass: the ranks share one GPU"
+    if not (args.no_cfg23 or args.no_cfg2) and not cpu_hook:
         out["cfg2"] = cfg2_block(fa_hip, dist)
     if not args.no_cfg4:
         out["cfg4"] = cfg4_block(fa_hip, world, rank, dist, args.cfg4_steps, 1, cpu_hook)
