@@ -1069,11 +1069,7 @@ __device__ __forceinline__ u32x4 desc_of(const void* base, uint32_t bytes) {
 __device__ __forceinline__ void dma16_asm(const u32x4& desc, uint32_t lds_base, int voff) {
     // s_nop 4: five wait states between a VALU write of the descriptor SGPRs (v_readlane
     // of a spilled SGPR, which the hazard recognizer cannot see past the asm) and the read
-#ifdef FA_BWD_DMA_POL   // experiments: cache policy of the loop's Q / dO DMA (e.g. "nt")
-    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen " FA_BWD_DMA_POL " lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
-#else
     asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff), "s"(desc), "{m0}"(lds_base) : "memory");
-#endif
 }
 template <int OFF>
 __device__ __forceinline__ u32x4 load16_sc1_asm(const u32x4& desc, int voff) {
