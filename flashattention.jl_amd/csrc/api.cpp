@@ -214,11 +214,12 @@ int fa_debug_set_circ_generic(int v) {
 // Not part of the public header: windowed forward path override (1 composed,
 // 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window
 // row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the auto choice at ws <= 7),
-// 10 eight-window strip (stride == ws), where eligible; 0 auto).  Modes 7-9 (rejected
+// 10 eight-window strip (stride == ws), 12 three-window row-shift, where eligible; 13: the
+// per-window backward with two windows per workgroup; 0 auto).  Modes 7-9 (rejected
 // experimental kernels) were removed; they now select the auto path.
 int fa_debug_set_win_composed(int v) {
     const int old = fa::g_win_force_composed;
-    fa::g_win_force_composed = ((v >= 1 && v <= 6) || v == 10) ? v : 0;
+    fa::g_win_force_composed = ((v >= 1 && v <= 6) || v == 10 || v == 12 || v == 13) ? v : 0;
     return old;
 }
 

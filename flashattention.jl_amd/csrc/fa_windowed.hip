@@ -1367,47 +1367,63 @@ __global__ __launch_bounds__(512, 2) void win_strip(const T* __restrict__ q, con
 //              image); each lane stores one slot's features straight to its pixel.
 // Padding slots (tx or ty >= ws): keys masked (P = dS = 0), queries have lse = +inf.
 // --------------------------------------------------------------------------
-template <class T, int D, int DV>
-__global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, const T* __restrict__ k,
+template <class T, int D, int DV, int NWIN>
+__global__ __launch_bounds__(256 * NWIN) void win_bwd_rows(const T* __restrict__ q, const T* __restrict__ k,
                                                     const T* __restrict__ v, const T* __restrict__ y,
                                                     const T* __restrict__ dy, const float* __restrict__ lw,
                                                     const float* __restrict__ mw, T* __restrict__ dq,
                                                     T* __restrict__ dk, T* __restrict__ dvo, WinDev g, int d,
-                                                    int dv, float scale, float scale_log2) {
+                                                    int dv, int nwin_total, float scale, float scale_log2) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
-    constexpr int NTH = 256, KROW = 128, PROW = 144;
+    constexpr int NTH = 256 * NWIN, KROW = 128, PROW = 144;
     constexpr int QIMG = D * KROW, VIMG = DV * KROW, PIMG = 64 * PROW;
     constexpr int OQ = 0, OK_ = QIMG, OV = 2 * QIMG, ODO = 2 * QIMG + VIMG, OP = 2 * QIMG + 2 * VIMG,
                   ODS = OP + PIMG, OLSE = ODS + PIMG, OD = OLSE + 256, REGION = OD + 4 * 256;
-    constexpr int NIQ = D * 8 / NTH, NIV = DV * 8 / NTH;
-    static_assert(D * 8 % NTH == 0 && DV * 8 % NTH == 0, "item split");
-    __shared__ __attribute__((aligned(16))) char smem[REGION];
+    constexpr int NIQ = D * 8 / 256, NIV = DV * 8 / 256;    // items per thread: window x feature x 8 slot rows
+    static_assert(D * 8 % 256 == 0 && DV * 8 % 256 == 0, "item split");
+    __shared__ __attribute__((aligned(16))) char smem[NWIN * REGION];
     auto kswz = [](int f) { return ((f >> 1) & 1) << 1; };
-    float* const lse_s = (float*)(smem + OLSE);   // −lse/τ per query slot (raw score units)
-    float* const dsum = (float*)(smem + OD);      // D per query slot: one partial per key half [2][64]
 
     FA_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W_ = g.S[0], H_ = g.S[1], P_ = g.P, ws = g.ws, st = g.stride;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int wx = bid % g.O[0], wy = (bid / g.O[0]) % g.O[1], b = bid / (g.O[0] * g.O[1]);
-    const int xs = wx * st - g.pad, y0 = wy * st - g.pad;
-    const int ax = min(max(xs & ~1, 0), W_ - 8);
-    const int sh = xs - ax;
-    const int64_t wid = (int64_t)(wx + g.O[0] * wy) + (int64_t)g.L * b;
-
-    auto item_off = [&](int it, int C) {
-        const int yy = it & 7, f = it >> 3, yr = y0 + yy;
-        const bool ok = yy < ws && yr >= 0 && yr < H_ && f < C;
-        return ok ? (f * P_ + yr * W_ + ax) * 2 : 0x7FFFFFF0;
+    // NWIN horizontally adjacent windows (xcd_remap: contiguous runs per XCD), 4 waves each
+    const int nperimg = g.O[0] * g.O[1];
+    struct Win { int wx, wy, b, xs, y0, ax; bool ok; };
+    auto win_of = [&](int wl) {
+        Win w;
+        const int id = xcd_remap(blockIdx.x, gridDim.x) * NWIN + wl;   // 32-bit: the host keeps L·B < 2^31
+        w.ok = id < nwin_total;
+        const int idc = w.ok ? id : 0;
+        w.b = idc / nperimg;
+        const int rem = idc - w.b * nperimg;
+        w.wy = rem / g.O[0];
+        w.wx = rem - w.wy * g.O[0];
+        w.xs = w.wx * st - g.pad;
+        w.y0 = w.wy * st - g.pad;
+        w.ax = min(max(w.xs & ~1, 0), W_ - 8);
+        return w;
     };
-    const auto qrs = slab_rsrc(q + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto krs = slab_rsrc(k + (int64_t)b * d * P_, (uint32_t)(d * P_ * 2));
-    const auto vrs = slab_rsrc(v + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    // staging item it -> (window it % NWIN, feature (it / NWIN) >> 3, slot row (it / NWIN) & 7): the
+    // NWIN windows' loads of one (feature, row) sit on adjacent lanes, 2·ws bytes apart, and share
+    // their cache lines; every item of a lane belongs to window tid % NWIN (NTH % NWIN == 0).
+    // Descriptors span the first window's image and the next (a pair may straddle images).
+    const int b0 = win_of(0).b;
+    const int nimg = min(NWIN == 1 ? 1 : 2, nwin_total / nperimg - b0);
+    const int wl_me = NWIN == 1 ? 0 : (int)(tid % NWIN);
+    const Win wme = win_of(wl_me);
+    auto item_off = [&](int it, int C) {
+        const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3, yr = wme.y0 + yy;
+        const bool ok = wme.ok && yy < ws && yr >= 0 && yr < H_ && f < C;
+        return ok ? (((wme.b - b0) * C + f) * P_ + yr * W_ + wme.ax) * 2 : 0x7FFFFFF0;
+    };
+    const auto qrs = slab_rsrc(q + (int64_t)b0 * d * P_, (uint32_t)(nimg * d * P_ * 2));
+    const auto krs = slab_rsrc(k + (int64_t)b0 * d * P_, (uint32_t)(nimg * d * P_ * 2));
+    const auto vrs = slab_rsrc(v + (int64_t)b0 * dv * P_, (uint32_t)(nimg * dv * P_ * 2));
     (void)y;
-    const auto drs = slab_rsrc(dy + (int64_t)b * dv * P_, (uint32_t)(dv * P_ * 2));
+    const auto drs = slab_rsrc(dy + (int64_t)b0 * dv * P_, (uint32_t)(nimg * dv * P_ * 2));
     u32x4 rq[NIQ], rk[NIQ], rv[NIV], rd[NIV];
 #pragma unroll
     for (int j = 0; j < NIQ; ++j) {
@@ -1421,51 +1437,83 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         rv[j] = __builtin_amdgcn_raw_buffer_load_b128(vrs, o, 0, 0);
         rd[j] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
     }
-    // per-slot constant −lse/τ (+inf lse outside the window)
-    if (tid < 64) {
-        const int tx = tid & 7, ty = tid >> 3;
+    // per-slot constant −lse/τ of window tid >> 6 (+inf lse outside the window)
+    if (tid < 64 * NWIN) {
+        const int wl = tid >> 6, tx = tid & 7, ty = (tid >> 3) & 7;
+        const Win w = win_of(wl);
         float nl = kNegInf;
-        if (tx < ws && ty < ws) {
+        if (w.ok && tx < ws && ty < ws) {
+            const int64_t wid = (int64_t)(w.wx + g.O[0] * w.wy) + (int64_t)g.L * w.b;
             const int64_t li = ty * ws + tx + (int64_t)g.T * wid;
             nl = -(mw[li] + __logf(lw[li])) / scale;
         }
-        lse_s[tid] = nl;
+        ((float*)(smem + wl * REGION + OLSE))[tid & 63] = nl;
     }
     unsigned mask[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int t0 = 2 * j, t1 = 2 * j + 1;
-        const bool v0 = t0 < ws && xs + t0 >= 0 && xs + t0 < W_;
-        const bool v1 = t1 < ws && xs + t1 >= 0 && xs + t1 < W_;
+        const bool v0 = t0 < ws && wme.xs + t0 >= 0 && wme.xs + t0 < W_;
+        const bool v1 = t1 < ws && wme.xs + t1 >= 0 && wme.xs + t1 < W_;
         mask[j] = (v0 ? 0x0000FFFFu : 0u) | (v1 ? 0xFFFF0000u : 0u);
     }
+    const int sh_me = wme.xs - wme.ax;
+    // NWIN > 1: lanes of a wave shift by different amounts; away from the image's left and
+    // right edges every shift is 0 or 1 pixel (one v_alignbyte per dword), as in win_rows1s
+    const bool near_shift = NWIN > 1 && __builtin_amdgcn_ballot_w64((sh_me >> 1) != 0) == 0;
+    const unsigned ab_me = (sh_me & 1) ? 2u : 0u;
+    char* const sme = smem + wl_me * REGION;
     auto koff = [&](int it) {
-        const int yy = it & 7, f = it >> 3;
+        const int rest = NWIN == 1 ? it : it / NWIN, yy = rest & 7, f = rest >> 3;
         return f * KROW + (((yy >> 1) ^ kswz(f)) * 32) + (yy & 1) * 16;
     };
+    auto stage_all = [&](auto fast) {
+        auto shifted = [&](const u32x4& val) {
+            u32x4 o;
+            if constexpr (NWIN == 1) {
+                o = shift_row(val, sh_me, mask);
+            } else if constexpr (decltype(fast)::value) {
 #pragma unroll
-    for (int j = 0; j < NIQ; ++j) {
-        const int o = koff(tid + NTH * j);
-        *(u32x4*)(smem + OQ + o) = shift_row(rq[j], sh, mask);
-        *(u32x4*)(smem + OK_ + o) = shift_row(rk[j], sh, mask);
-    }
-    FA_STAMP(1);
+                for (int j = 0; j < 4; ++j)
+                    o[j] = __builtin_amdgcn_alignbyte(j < 3 ? val[j + 1] : 0u, val[j], ab_me) & mask[j];
+            } else {
+                o = shift_row_lane(val, sh_me, mask);
+            }
+            return o;
+        };
 #pragma unroll
-    for (int j = 0; j < NIV; ++j) {
-        const int o = koff(tid + NTH * j);
-        *(u32x4*)(smem + OV + o) = shift_row(rv[j], sh, mask);
-        *(u32x4*)(smem + ODO + o) = shift_row(rd[j], sh, mask);
-    }
+        for (int j = 0; j < NIQ; ++j) {
+            const int o = koff(tid + NTH * j);
+            *(u32x4*)(sme + OQ + o) = shifted(rq[j]);
+            *(u32x4*)(sme + OK_ + o) = shifted(rk[j]);
+        }
+        FA_STAMP(1);
+#pragma unroll
+        for (int j = 0; j < NIV; ++j) {
+            const int o = koff(tid + NTH * j);
+            *(u32x4*)(sme + OV + o) = shifted(rv[j]);
+            *(u32x4*)(sme + ODO + o) = shifted(rd[j]);
+        }
+    };
+    if (near_shift) stage_all(std::true_type{});
+    else stage_all(std::false_type{});
     __syncthreads();
     FA_STAMP(2);
 
+    // ---- this wave's window ----
+    const Win w = win_of(wave >> 2);
+    char* const wsm = smem + (wave >> 2) * REGION;
+    const int b = w.b, xs = w.xs, y0 = w.y0;
+    float* const lse_s = (float*)(wsm + OLSE);   // −lse/τ per query slot (raw score units)
+    float* const dsum = (float*)(wsm + OD);      // D per query slot: one partial per key half [2][64]
+
     // ---- phase 1: S and dP blocks (qb, kb) of this wave ----
-    const int qb = wave & 1, kb = wave >> 1;
+    const int qb = wave & 1, kb = (wave >> 1) & 1;
     const int g4 = lane >> 4, kh = g4 & 1, qq = (lane & 15) >> 2, pp = lane & 3;
     // tr-read of a [feature][slot] image: 32 slots of block sb, features 16 s + 8 h .. + 7
     auto frag_tr = [&](int img, int sb, int s16) {
         const int orow = (16 * s16 + 8 * h + qq) * KROW;
-        const char* a = smem + img + orow + (((sb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
+        const char* a = wsm + img + orow + (((sb * 2 + kh) ^ kswz(qq)) * 32) + 8 * pp;
         return __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
                                        __builtin_bit_cast(F4, ds_read_tr16(a + 4 * KROW)), 0, 1, 2, 3, 4, 5, 6, 7);
     };
@@ -1493,7 +1541,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
             pr[4 * x4 + e] = kvalid ? exp2_fast(sa[4 * x4 + e] * scale_log2) : 0.0f;
             p4[e] = (T)pr[4 * x4 + e];
         }
-        *(typename Frag8<T>::half*)(smem + OP + kslot * PROW + (qb * 32 + acc_row(4 * x4, h)) * 2) = p4;
+        *(typename Frag8<T>::half*)(wsm + OP + kslot * PROW + (qb * 32 + acc_row(4 * x4, h)) * 2) = p4;
     }
 #pragma unroll
     for (int x = 0; x < 16; ++x) {
@@ -1515,7 +1563,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
         typename Frag8<T>::half s4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) s4[e] = (T)(pr[4 * x4 + e] * (pa[4 * x4 + e] - d4[e]));
-        *(typename Frag8<T>::half*)(smem + ODS + kslot * PROW + qrow * 2) = s4;
+        *(typename Frag8<T>::half*)(wsm + ODS + kslot * PROW + qrow * 2) = s4;
     }
     lds_barrier();
     FA_STAMP(3);
@@ -1523,11 +1571,11 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     // ---- phase 2: dVᵀ, dKᵀ, dQᵀ blocks ----
     // row read: 8 consecutive slots 16 s + 8 h of feature row f of a [feature][slot] image
     auto frag_row = [&](int img, int f, int s16) {
-        return *(const F8*)(smem + img + f * KROW + ((s16 ^ kswz(f)) * 32) + 16 * h);
+        return *(const F8*)(wsm + img + f * KROW + ((s16 ^ kswz(f)) * 32) + 16 * h);
     };
     auto store_px = [&](T* out, int C, int slot, int fbase, const f32x16& acc, float mul) {
         const int tx = slot & 7, ty = slot >> 3, px = xs + tx, py = y0 + ty;
-        if (tx < ws && ty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
+        if (w.ok && tx < ws && ty < ws && px >= 0 && px < W_ && py >= 0 && py < H_) {
             T* ob = out + (int64_t)b * C * P_ + (int64_t)py * W_ + px;
 #pragma unroll
             for (int x = 0; x < 16; ++x) {
@@ -1539,7 +1587,7 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
     constexpr int NDV = DV / 32 * 2, NDK = D / 32 * 2, NBLK = NDV + 2 * NDK;
 #pragma unroll
     for (int i = 0; i < (NBLK + 3) / 4; ++i) {
-        const int blk = wave + 4 * i;
+        const int blk = (wave & 3) + 4 * i;
         if (blk >= NBLK) break;
         f32x16 acc;
 #pragma unroll
@@ -1549,20 +1597,20 @@ __global__ __launch_bounds__(256) void win_bwd_rows(const T* __restrict__ q, con
 #pragma unroll
             for (int s16 = 0; s16 < 4; ++s16)
                 acc = mfma32x32x16(frag_row(ODO, f, s16),
-                                   *(const F8*)(smem + OP + (kb2 * 32 + r) * PROW + (16 * s16 + 8 * h) * 2), acc);
+                                   *(const F8*)(wsm + OP + (kb2 * 32 + r) * PROW + (16 * s16 + 8 * h) * 2), acc);
             store_px(dvo, dv, kb2 * 32 + r, cb * 32, acc, 1.0f);
         } else if (blk < NDV + NDK) {                 // dKᵀ[fb, kb2] = τ Qᵀ dS
             const int b2 = blk - NDV, fb = b2 >> 1, kb2 = b2 & 1, f = fb * 32 + r;
 #pragma unroll
             for (int s16 = 0; s16 < 4; ++s16)
                 acc = mfma32x32x16(frag_row(OQ, f, s16),
-                                   *(const F8*)(smem + ODS + (kb2 * 32 + r) * PROW + (16 * s16 + 8 * h) * 2), acc);
+                                   *(const F8*)(wsm + ODS + (kb2 * 32 + r) * PROW + (16 * s16 + 8 * h) * 2), acc);
             store_px(dk, d, kb2 * 32 + r, fb * 32, acc, scale);
         } else {                                      // dQᵀ[fb, qb2] = τ Kᵀ dSᵀ
             const int b2 = blk - NDV - NDK, fb = b2 >> 1, qb2 = b2 & 1, f = fb * 32 + r;
 #pragma unroll
             for (int s16 = 0; s16 < 4; ++s16) {
-                const char* a = smem + ODS + (16 * s16 + 8 * h + qq) * PROW + (qb2 * 32 + kh * 16 + 4 * pp) * 2;
+                const char* a = wsm + ODS + (16 * s16 + 8 * h + qq) * PROW + (qb2 * 32 + kh * 16 + 4 * pp) * 2;
                 const F8 bt = __builtin_shufflevector(__builtin_bit_cast(F4, ds_read_tr16(a)),
                                                       __builtin_bit_cast(F4, ds_read_tr16(a + 4 * PROW)),
                                                       0, 1, 2, 3, 4, 5, 6, 7);
@@ -2598,6 +2646,10 @@ static bool strip_applies(int dtype, const WindowGeom& g, int64_t d, int64_t dv,
     return g_win_force_composed == 10 || nstrip >= kStripMin;
 }
 
+// Window counts between which the row-shift forward runs three windows per workgroup
+// (768 threads) instead of two.
+constexpr int64_t kRows3Min = 600, kRows3Max = 1000;
+
 template <class T, int D, int DV>
 static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStream_t s) {
     if (a.g.ws <= 7 && g_win_force_composed != 5) {
@@ -2611,7 +2663,18 @@ static hipError_t launch_rows1_dd(const WindowedArgs& a, const WinDev& g, hipStr
             return hipGetLastError();
         }
         const bool two_img_ok = 2 * a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX;
-        if (g_win_force_composed != 3 && two_img_ok) {   // default: register-staged, two windows per workgroup
+        // three windows per workgroup on mid-size grids (round 6, profiles/r06_win_nwin_ab.log,
+        // configs[2] shape: B = 2 8.09-8.14 vs 8.82-8.95 us, B = 3 11.67 vs 11.41, B = 4 a tie, B = 1
+        // 7.10 vs 6.23, r06_win_nwin_ab2.log; four windows
+        // per workgroup slower at every B): fewer, longer workgroups than two windows give,
+        // with one more window's row loads coalesced per (feature, row) line
+        const bool three = g_win_force_composed == 12 ||
+                           (g_win_force_composed == 0 && nw >= kRows3Min && nw < kRows3Max);
+        if (three && two_img_ok) {
+            hipLaunchKernelGGL((win_rows1s<T, D, DV, 3>), dim3((unsigned)((nw + 2) / 3)), dim3(768), 0, s,
+                               (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
+                               (int)a.dv, nw, a.scale, a.scale * kLog2e);
+        } else if (g_win_force_composed != 3 && two_img_ok) {   // default: register-staged, two windows per workgroup
             hipLaunchKernelGGL((win_rows1s<T, D, DV, 2>), dim3((unsigned)((nw + 1) / 2)), dim3(512), 0, s,
                                (const T*)a.q, (const T*)a.k, (const T*)a.v, (T*)a.y, a.l, a.m, g, (int)a.d,
                                (int)a.dv, nw, a.scale, a.scale * kLog2e);
@@ -2926,12 +2989,15 @@ static bool bwd_rows_ok(const WindowedBwdArgs& a) {
                     ((uintptr_t)a.y & 15u) == 0 && ((uintptr_t)a.dy & 15u) == 0;
     return g_win_force_composed != 1 && (a.dtype == FA_DTYPE_BF16 || a.dtype == FA_DTYPE_F16) && a.g.nsp == 2 && a.g.stride >= a.g.ws &&
            a.g.ws <= 7 && a.g.S[0] % 8 == 0 && a.d <= 128 && a.dv <= 128 && al &&
-           a.g.P * 128 * 2 < INT32_MAX;
+           a.g.P * 128 * 2 < INT32_MAX && a.g.L * a.batch < INT32_MAX;
 }
 
 // The strip backward (win_bwd_strip): the forward strip kernel's shapes, d, dv <= 64,
 // 16-B aligned gradients too; from kStripBwdMin strips on (or forced by mode 10).
 constexpr int64_t kStripBwdMin = 256;
+// The per-window backward pairs windows up to this many windows per CU (1.5: configs[2] at
+// B = 1 is 361 windows on 256 CUs).
+constexpr double kBwdPairMaxPerCu = 1.5;
 static bool bwd_strip_ok(const WindowedBwdArgs& a) {
     auto al = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
     if ((a.dtype != FA_DTYPE_BF16 && a.dtype != FA_DTYPE_F16) || a.g.nsp != 2 || a.g.stride != a.g.ws || a.g.ws > 7 ||
@@ -2998,14 +3064,29 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
         }
         return FA_OK;
     }
-    const dim3 grid((unsigned)(a.g.L * a.batch));
-#define FA_BWD_ROWS(DD, DVV)                                                                                 hipLaunchKernelGGL((win_bwd_rows<T, DD, DVV>), grid, dim3(256), 0, s, (const T*)a.q, (const T*)a.k,                         (const T*)a.v, (const T*)a.y, (const T*)a.dy, a.l, a.m, (T*)a.dq, (T*)a.dk,                              (T*)a.dv_, g, (int)a.d, (int)a.dv, a.scale, a.scale * kLog2e)
+    const int64_t nw = a.g.L * a.batch;
+    // two adjacent windows per workgroup (their row loads share lines, as in win_rows1s) while
+    // the grid is at most about one round of CUs; one window per workgroup, several per CU,
+    // above it (round 6)
+    const int64_t cus = device_cus(s) > 0 ? device_cus(s) : 256;
+    const bool pair = a.d <= 64 && a.dv <= 64 && 2 * a.g.P * (a.d > a.dv ? a.d : a.dv) * 2 < INT32_MAX &&
+                      (g_win_force_composed == 13 || (g_win_force_composed == 0 && nw <= kBwdPairMaxPerCu * cus));
+#define FA_BWD_ROWS(DD, DVV, NW)                                                                               \
+    hipLaunchKernelGGL((win_bwd_rows<T, DD, DVV, NW>), dim3((unsigned)((nw + NW - 1) / NW)), dim3(256 * NW), 0, s,  \
+                       (const T*)a.q, (const T*)a.k, (const T*)a.v, (const T*)a.y, (const T*)a.dy, a.l, a.m,       \
+                       (T*)a.dq, (T*)a.dk, (T*)a.dv_, g, (int)a.d, (int)a.dv, (int)nw, a.scale, a.scale * kLog2e)
     const int Dc = a.d <= 32 ? 32 : 64, DVc = a.dv <= 32 ? 32 : 64;
-    if (a.d > 64 || a.dv > 64) FA_BWD_ROWS(128, 128);   // 83 KB of LDS: one workgroup per CU
-    else if (Dc == 32 && DVc == 32) FA_BWD_ROWS(32, 32);
-    else if (Dc == 32) FA_BWD_ROWS(32, 64);
-    else if (DVc == 32) FA_BWD_ROWS(64, 32);
-    else FA_BWD_ROWS(64, 64);
+    if (a.d > 64 || a.dv > 64) FA_BWD_ROWS(128, 128, 1);   // 83 KB of LDS: one workgroup per CU
+    else if (pair) {
+        if (Dc == 32 && DVc == 32) FA_BWD_ROWS(32, 32, 2);
+        else if (Dc == 32) FA_BWD_ROWS(32, 64, 2);
+        else if (DVc == 32) FA_BWD_ROWS(64, 32, 2);
+        else FA_BWD_ROWS(64, 64, 2);
+    }
+    else if (Dc == 32 && DVc == 32) FA_BWD_ROWS(32, 32, 1);
+    else if (Dc == 32) FA_BWD_ROWS(32, 64, 1);
+    else if (DVc == 32) FA_BWD_ROWS(64, 32, 1);
+    else FA_BWD_ROWS(64, 64, 1);
 #undef FA_BWD_ROWS
     if ((e = hipGetLastError()) != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -86,3 +86,30 @@ def test_config3_full_size(fa):
     assert_close(_np(y), yr, "bfloat16", "y", nan_ok=True)
     assert_lm_close(_np(l), lr, "bfloat16", "l")
     assert_lm_close(_np(m), mr, "bfloat16", "m")
+
+
+@pytest.mark.parametrize("B,mode", [(1, 0), (1, 3), (3, 13)])
+def test_config2_backward_full_size_window_pairing(fa, B, mode):
+    """BASELINE configs[2] backward on the full image against the oracle's chain rule,
+    through the per-window kernel with two windows per workgroup (auto at B = 1: 361
+    windows; forced at B = 3, where a pair straddles two images since 361 is odd) and
+    with one (mode 3); the two layouts give the same bits."""
+    rng = np.random.default_rng(17 + B)
+    bf = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()
+    q, k, v, dy = (bf(rng.standard_normal((128, 128, 64, B))) for _ in range(4))
+    Q, K, V, DY = (fa.jl_tensor(a, torch.bfloat16) for a in (q, k, v, dy))
+    y, l, m = fa.windowed_fa(Q, K, V, 7)
+    L = fa.lib()
+    grads = {}
+    for md in (mode, 3):
+        old = L.fa_debug_set_win_composed(md)
+        try:
+            grads[md] = [t.clone() for t in fa.windowed_fa_backward(Q, K, V, y, DY, l, m, 7)]
+            torch.cuda.synchronize()
+        finally:
+            L.fa_debug_set_win_composed(old)
+    for a, b_ in zip(grads[mode], grads[3]):
+        assert torch.equal(a, b_), "window pairing changed the bits"
+    ref = O.windowed_fa_backward(q, k, v, dy, 7, 7, 3)
+    for a, b_, nm in zip(grads[mode], ref, ("dq", "dk", "dv")):
+        assert_close(_np(a), b_, "bfloat16", nm)

@@ -1,7 +1,7 @@
 """GPU parity of every fused windowed-forward kernel, each forced in turn
 (fa_debug_set_win_composed: 1 composed gather→dense→fold, 2 register-gather,
 3 one-window row-shift (ws <= 7) / row-scatter (ws = 8), 4 four-window
-row-staged, 5 one-window row-scatter, 6 two-window row-shift, 10 the eight-window strip kernel
+row-staged, 5 one-window row-scatter, 6 two-window row-shift, 12 three-window row-shift, 10 the eight-window strip kernel
 with rotated slots and analytic padding columns), against the oracle restatement of
 windowed_fa (src/windowed.jl:3-23, NNlib unfold/fold geometry) on geometries
 chosen for the row-staged kernels' edge handling: windows hanging over the
@@ -45,7 +45,7 @@ def _np(t):
     return t.detach().float().cpu().numpy().astype(np.float64)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 10])
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5, 6, 10, 12])
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "W{}H{}ws{}s{}p{}".format(*g))
 def test_windowed_forced_path(fa, geom, path):
     W, H, ws, st, pad = geom
@@ -186,7 +186,7 @@ def test_windowed_backward_f32_paths(fa, geom, path):
         L.fa_debug_set_win_composed(old)
 
 
-@pytest.mark.parametrize("path", [0, 3, 6, 10])
+@pytest.mark.parametrize("path", [0, 3, 6, 10, 12])
 def test_windowed_nonfinite_stays_in_its_window(fa, path):
     """An inf in one pixel's k and v reaches only the window holding that pixel, as in
     the reference, where windows are disjoint token sets.  The fused kernels load 8-pixel

@@ -10,8 +10,8 @@ import fa_hip
 from bench import time_graph
 L = fa_hip.lib()
 L.fa_debug_set_win_composed.argtypes = [ctypes.c_int]
-NAMES = {0: "auto    ", 3: "rows1   ", 6: "rows1x2 ", 4: "rows4   ", 2: "gather  ", 1: "composed", 7: "dma2    ",
-         10: "strip8  "}
+NAMES = {0: "auto    ", 3: "rows1   ", 6: "rows1x2 ", 4: "rows4   ", 2: "gather  ", 1: "composed",
+         10: "strip8  ", 12: "rows1x3 "}
 MODES = [int(x) for x in os.environ.get("WMODES", "0,3,6,4,2").split(",")]
 Bs = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8, 32, 128]
 for B in Bs:
@@ -19,14 +19,19 @@ for B in Bs:
     q, k, v = (fa_hip.jl_tensor(torch.randn((128, 128, 64, B), generator=g, device="cuda"), torch.bfloat16) for _ in range(3))
     T, Lw = 49, 361
     alg = B * (4 * 128 * 128 * 64 * 2 + 2 * T * Lw * 4)
-    res = {}
+    res, ts = {}, {c: [] for c in MODES}
     for comp in MODES:
         L.fa_debug_set_win_composed(comp)
         y, l, m = fa_hip.windowed_fa(q, k, v, 7)
         torch.cuda.synchronize()
         res[comp] = (y.float(), l.clone())
-        t = time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), 20)
-        print(f"B={B:4d} {NAMES[comp]}: {t*1e6:9.1f} us  {alg/t/1e9:8.1f} GB/s", flush=True)
+    for rnd in range(int(os.environ.get("WROUNDS", 1))):   # interleaved rounds, median reported
+        for comp in MODES:
+            L.fa_debug_set_win_composed(comp)
+            ts[comp].append(time_graph(lambda: fa_hip.windowed_fa(q, k, v, 7), 20))
+    for comp in MODES:
+        t = sorted(ts[comp])[len(ts[comp]) // 2]
+        print(f"B={B:4d} {NAMES[comp]}: {t*1e6:9.2f} us  {alg/t/1e9:8.1f} GB/s  (min {min(ts[comp])*1e6:.2f})", flush=True)
     ref = MODES[-1]
     for c in MODES[:-1]:
         dy = (res[c][0] - res[ref][0]).abs().max()
