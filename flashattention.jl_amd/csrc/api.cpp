@@ -223,6 +223,14 @@ int fa_debug_set_win_composed(int v) {
     return old;
 }
 
+// Not part of the public header: workgroups of the persistent strip backward (0 = one per
+// CU, the default; 1..4096 caps the grid).  Benchmark knob; returns the previous value.
+int fa_debug_set_win_bwd_grid(int v) {
+    const int old = fa::g_win_bwd_grid;
+    if (v >= 0 && v <= 4096) fa::g_win_bwd_grid = v;
+    return old;
+}
+
 size_t fa_dense_fwd_workspace(int dtype, int64_t N, int64_t Nk, int64_t d, int64_t dv, int64_t batch) {
     if (!valid_dtype(dtype) || N < 1 || Nk < 1 || d < 1 || dv < 1 || batch < 1) return 0;
     return fa::dense_fwd_workspace(dtype, N, Nk, d, dv, batch);

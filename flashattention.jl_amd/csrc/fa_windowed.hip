@@ -2576,6 +2576,9 @@ static bool rows_f32_ok(const WindowedArgs& a) {
            a.g.P * (a.d > a.dv ? a.d : a.dv) * 4 < INT32_MAX - 64;
 }
 
+#if FA_WIN_PART != 1
+thread_local int g_win_bwd_grid = 0;   // benchmark knob: the strip backward's workgroups (0: one per CU)
+#endif
 #if FA_WIN_PART != 2
 thread_local int g_win_force_composed = 0;   // benchmark knob: 1 composed, 2 register-gather fused, 3 one-window row-shift (ws <= 7) / row-scatter, 4 four-window row-scatter, 5 one-window row-scatter, 6 two-window row-shift (the default for small launches), 10 eight-window strip (the default from kStripMin strips on); modes 7-9 (the rejected LDS-DMA and segment kernels) were removed in round 4
 #endif
@@ -3026,7 +3029,8 @@ static int windowed_bwd_rows(const WindowedBwdArgs& a, hipStream_t s, const char
         const int64_t nsx = strip_count(a.g, k0), nstrip = nsx * a.g.O[1] * a.batch;
         // persistent: one workgroup per CU, strips dealt by 8 XCD-group counters in the workspace
         const int64_t cus = device_cus(s) > 0 ? device_cus(s) : 256;
-        const int64_t grid = nstrip < cus ? nstrip : cus;
+        const int64_t gmax = g_win_bwd_grid > 0 ? (int64_t)g_win_bwd_grid : cus;
+        const int64_t grid = nstrip < gmax ? nstrip : gmax;
         // the counters are atomic words: round their address up to 256 B as the dense
         // backward does (the header allows any workspace alignment; windowed_workspace
         // reserves the 256-B slack, and its buffers are far larger than the 512 B used)
