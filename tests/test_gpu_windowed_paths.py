@@ -402,3 +402,29 @@ def test_windowed_backward_strip_dynamic_deal_every_image(fa, B):
         assert torch.isfinite(x).all(), f"{nm}: non-finite gradient (a strip not computed?)"
         per_image = ((x - xr).abs().amax(dim=(0, 1, 2)) / xr.abs().amax(dim=(0, 1, 2)).clamp_min(1e-2))
         assert float(per_image.max()) <= 2e-2, f"{nm}: worst image {int(per_image.argmax())} err {float(per_image.max()):.2e}"
+
+
+@pytest.mark.parametrize("grid", [37, 200, 257])
+def test_windowed_backward_strip_deal_any_grid(fa, grid):
+    """The strip backward's XCD-group deal at grid sizes other than one workgroup per CU
+    (fa_debug_set_win_bwd_grid: 37 leaves groups of 4 and 5 workgroups, 200 an uneven
+    split over the 8 groups, 257 is capped at the strip count's grid rule only): every
+    strip is computed exactly once, so the gradients are bitwise those of the default grid."""
+    import ctypes
+    W = H = 128
+    B, d = 8, 64
+    g = torch.Generator(device="cuda").manual_seed(90 + grid)
+    q, k, v, dy = (fa.jl_tensor(torch.randn((W, H, d, B), generator=g, device="cuda"), torch.bfloat16)
+                   for _ in range(4))
+    y, l, m = fa.windowed_fa(q, k, v, 7)
+    ref = [t.clone() for t in fa.windowed_fa_backward(q, k, v, y, dy, l, m, 7)]
+    L = fa.lib()
+    L.fa_debug_set_win_bwd_grid.argtypes = [ctypes.c_int]
+    old = L.fa_debug_set_win_bwd_grid(grid)
+    try:
+        out = fa.windowed_fa_backward(q, k, v, y, dy, l, m, 7)
+        torch.cuda.synchronize()
+    finally:
+        L.fa_debug_set_win_bwd_grid(old)
+    for a, r, nm in zip(out, ref, ("dq", "dk", "dv")):
+        assert torch.equal(a, r), f"grid {grid} {nm}: differs from the default grid"

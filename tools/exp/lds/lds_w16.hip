@@ -1,0 +1,47 @@
+// Microbenchmark: LDS write cost of ds_write_b16 with adjacent lanes writing the two halves of
+// one dword (the strip images' pattern) vs ds_write_b16 to distinct dwords vs ds_write_b32.
+// One workgroup of 512 threads per CU, every wave loops; cycles per wave-instruction.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+template <int MODE>
+__global__ __launch_bounds__(512) void k(unsigned long long* out, int iters) {
+    __shared__ __attribute__((aligned(16))) char sm[65536];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned a;
+    if (MODE == 0) a = (wave * 8192) + lane * 2;            // b16, lanes 2i / 2i+1 share a dword
+    else if (MODE == 1) a = (wave * 8192) + lane * 4;       // b16, one dword per lane
+    else a = (wave * 8192) + lane * 4;                      // b32, one dword per lane
+    unsigned v = threadIdx.x;
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (MODE == 2) asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(a), "v"(v), "i"(j * 512) : "memory");
+            else asm volatile("ds_write_b16 %0, %1 offset:%2" : : "v"(a), "v"(v), "i"(j * 512) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x * 8 + wave] = t1 - t0;
+}
+int main() {
+    unsigned long long* d; hipMalloc(&d, 256 * 8 * 8);
+    unsigned long long h[256 * 8];
+    const int iters = 2000;
+    const char* names[3] = {"b16 two lanes per dword", "b16 one dword per lane", "b32 one dword per lane"};
+    for (int rep = 0; rep < 2; ++rep)
+    for (int m = 0; m < 3; ++m) {
+        if (m == 0) hipLaunchKernelGGL(k<0>, dim3(256), dim3(512), 0, 0, d, iters);
+        if (m == 1) hipLaunchKernelGGL(k<1>, dim3(256), dim3(512), 0, 0, d, iters);
+        if (m == 2) hipLaunchKernelGGL(k<2>, dim3(256), dim3(512), 0, 0, d, iters);
+        hipDeviceSynchronize();
+        hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+        double s = 0; for (int i = 0; i < 256 * 8; ++i) s += h[i];
+        s /= 256 * 8;
+        // memtime ticks at the shader clock on gfx9 (s_memtime): cycles per wave per instruction,
+        // and per CU (8 waves share the LDS)
+        printf("%-26s: %.2f cycles per wave-instruction (%.2f per CU-instruction)\n", names[m], s / (iters * 16.0), s / (iters * 16.0 * 8));
+    }
+    return 0;
+}
