@@ -9,15 +9,23 @@ __global__ __launch_bounds__(512) void k(unsigned long long* out, int iters) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned a;
     if (MODE == 0) a = (wave * 8192) + lane * 2;            // b16, lanes 2i / 2i+1 share a dword
-    else if (MODE == 1) a = (wave * 8192) + lane * 4;       // b16, one dword per lane
-    else a = (wave * 8192) + lane * 4;                      // b32, one dword per lane
+    else if (MODE <= 3) a = (wave * 8192) + lane * 4;       // b16 / b32 / or_b32, one dword per lane
+    else if (MODE == 4) a = (wave * 8192) + lane * 8;       // b64
+    else a = (wave * 8192) + lane * 16;                     // b128 (wraps within 8 KB per wave: offsets below)
     unsigned v = threadIdx.x;
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    u4 v4 = {v, v, v, v};
+    u2 v2 = {v, v};
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             if (MODE == 2) asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(a), "v"(v), "i"(j * 512) : "memory");
+            else if (MODE == 3) asm volatile("ds_or_b32 %0, %1 offset:%2" : : "v"(a), "v"(v), "i"(j * 512) : "memory");
+            else if (MODE == 4) asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(a), "v"(v2), "i"((j & 7) * 512) : "memory");
+            else if (MODE == 5) asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(a & 8191), "v"(v4), "i"((j & 3) * 16384) : "memory");
             else asm volatile("ds_write_b16 %0, %1 offset:%2" : : "v"(a), "v"(v), "i"(j * 512) : "memory");
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -29,12 +37,16 @@ int main() {
     unsigned long long* d; hipMalloc(&d, 256 * 8 * 8);
     unsigned long long h[256 * 8];
     const int iters = 2000;
-    const char* names[3] = {"b16 two lanes per dword", "b16 one dword per lane", "b32 one dword per lane"};
+    const char* names[6] = {"b16 two lanes per dword", "b16 one dword per lane", "b32 one dword per lane",
+                            "or_b32 one dword per lane", "b64", "b128"};
     for (int rep = 0; rep < 2; ++rep)
-    for (int m = 0; m < 3; ++m) {
+    for (int m = 0; m < 6; ++m) {
         if (m == 0) hipLaunchKernelGGL(k<0>, dim3(256), dim3(512), 0, 0, d, iters);
         if (m == 1) hipLaunchKernelGGL(k<1>, dim3(256), dim3(512), 0, 0, d, iters);
         if (m == 2) hipLaunchKernelGGL(k<2>, dim3(256), dim3(512), 0, 0, d, iters);
+        if (m == 3) hipLaunchKernelGGL(k<3>, dim3(256), dim3(512), 0, 0, d, iters);
+        if (m == 4) hipLaunchKernelGGL(k<4>, dim3(256), dim3(512), 0, 0, d, iters);
+        if (m == 5) hipLaunchKernelGGL(k<5>, dim3(256), dim3(512), 0, 0, d, iters);
         hipDeviceSynchronize();
         hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
         double s = 0; for (int i = 0; i < 256 * 8; ++i) s += h[i];
