@@ -399,7 +399,7 @@ def cfg2_block(fa, dist, steps=20):
             "fwd_kernel": "fa::win_strip<bf16,64,64>" if Bimg >= 5 else "fa::win_rows1s<bf16,64,64,2>",
             "bwd_us": tb * 1e6, "bwd_GBs": bb / tb / 1e9, "bwd_frac_hbm": bb / tb / 1e9 / PEAK_HBM_GBS,
             "bwd_bytes": bb,
-            "bwd_kernel": "fa::win_bwd_strip<bf16,64,64>" if Bimg >= 5 else "fa::win_bwd_rows<bf16,64,64>"}
+            "bwd_kernel": "fa::win_bwd_strip<bf16,64,64>" if Bimg >= 5 else "fa::win_bwd_rows<bf16,64,64,2>"}
         del q, k, v, dy, y, lw, mw
     torch.cuda.empty_cache()
     return res
