@@ -1105,9 +1105,6 @@ __device__ __forceinline__ void vm_wait() {
     __builtin_amdgcn_s_waitcnt(0x0F70 | N);
 }
 
-#ifndef FA_BWD_STAG
-#define FA_BWD_STAG 0
-#endif
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     typedef typename Frag8<T>::type F8;
@@ -1366,117 +1363,6 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         look_next();
     }
 
-    // Staggered dQ (FA_BWD_STAG, d = 128): waves 4-7 (the dQᵀ tiles of queries 32..63)
-    // run a step's tile at the start of the next step, beside waves 0-3's phase A, and
-    // waves 0-3 run theirs right after their own phase A, beside waves 4-7's; the two
-    // waves of a SIMD are a tile apart instead of in lockstep.  LDS counters order the
-    // dSᵀ image: waves 0-3 read the u = 0 half once every wave has written it (s_u0),
-    // and no wave writes the u = 1 half before the late tiles have read the last one's (s_dq).
-    constexpr bool kStag = FA_BWD_STAG != 0 && D == 128;
-    const bool late = kStag && wave >= 4;
-    __shared__ unsigned s_u0, s_dq;
-    if (kStag && tid == 0) {
-        s_u0 = 0u;
-        s_dq = 0u;
-    }
-    // the late tile's slice (wave-uniform) and its running-sum input
-    int lt_t = 0, lt_pofs = 0;
-    bool lt_ldpin = false, lt_direct = false, lt_final = false, lt_plain = false;
-    u32x4 lpin[4] = {};
-    // dQᵀ tile (features 32 cbq.., queries 32 uq..) over the 256 keys into acc
-    auto dq_mfma = [&](f32x16& acc, int lq) {
-        const int rq = lq & 31, hq = lq >> 5;
-#pragma unroll
-        for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
-        uint32_t ka[4];
-        const int rswq = swz16(rq);
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4)
-            ka[q4] = lds_addr(kimg + (cbq * 32 + rq) * 128 + ((((q4 >> 1) * 4 + 2 * (q4 & 1) + hq) ^ rswq) * 16));
-        const int qqq = (lq & 15) >> 2, ppq = lq & 3, khq = (lq >> 4) & 1;
-        const int sgq = (ppq == 1) ? 2 : (ppq == 2) ? 1 : ppq;
-        const uint32_t da = lds_addr(dsimg + (8 * hq + qqq) * 128 +
-                                     (((uq * 4 + khq * 2 + (sgq >> 1)) ^ swzds(8 * hq + qqq)) * 16) + (sgq & 1) * 8);
-        u32x4 fa[2];
-        s16x4 flo[2], fhi[2];
-        auto issue = [&](auto kc) {
-            constexpr int kk = decltype(kc)::value;
-            fa[kk & 1] = lds_b128_at<(kk >> 2) * KSUB>(ka[kk & 3]);
-            flo[kk & 1] = lds_tr16_at<2048 * kk>(da);
-            fhi[kk & 1] = lds_tr16_at<2048 * kk + 512>(da);
-        };
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the reads below are counted by hand
-        issue(std::integral_constant<int, 0>{});
-        static_for<16>([&](auto kc) {
-            constexpr int kk = decltype(kc)::value;
-            if constexpr (kk + 1 < 16) {
-                issue(std::integral_constant<int, kk + 1>{});
-                lgkm_wait<3>();
-            } else {
-                lgkm_wait<0>();
-            }
-            reg_fence(fa[kk & 1]);
-            reg_fence(flo[kk & 1]);
-            reg_fence(fhi[kk & 1]);
-            const F4 lo = __builtin_bit_cast(F4, flo[kk & 1]);
-            const F4 hi = __builtin_bit_cast(F4, fhi[kk & 1]);
-            acc = mfma32x32x16(__builtin_bit_cast(F8, fa[kk & 1]), __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), acc);
-        });
-    };
-    // the tile's sums in, then dQ out (the chain's end) or the running sum on
-    auto dq_finish = [&](f32x16& acc, const u32x4 (&pn)[4], int tt, int pofs_, bool ldpin_, bool direct_, bool final_,
-                         bool plain_, int lq) {
-        const int rq = lq & 31, hq = lq >> 5;
-        if (ldpin_) {
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pn[c4][e]);
-        }
-        if (direct_) {
-            const int pofa = pofs_ - pchain4;
-            u32x4 pa[4];
-            pa[0] = load16_sc1_asm<0>(pdesc, pofa);
-            pa[1] = load16_sc1_asm<1024>(pdesc, pofa);
-            pa[2] = load16_sc1_asm<2048>(pdesc, pofa);
-            pa[3] = load16_sc1_asm<3072>(pdesc, pofa);
-            vm_wait<0>();
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-                reg_fence(pa[c4]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pa[c4][e]);
-            }
-        }
-        if (final_) {
-            const int q = tt * 64 + 32 * uq + sig32(rq);
-            const auto qo = bslab<T>(p.dQ, (int64_t)b * N * D, (int64_t)N * D);
-            const int vo = q < N ? ((cbq * 32 + 4 * hq) * N + q) * 2 : N * D * 2;   // past N: dropped
-#pragma unroll
-            for (int x = 0; x < 16; ++x)
-                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[x] * p.scale)), qo, vo,
-                                                      ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
-        } else {
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-                const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
-                                  __float_as_uint(acc[4 * c4 + 2]), __float_as_uint(acc[4 * c4 + 3])};
-                if (plain_) __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs_ + c4 * 1024, 0, 0);
-                else __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs_ + c4 * 1024, 0, 16);   // sc1
-            }
-        }
-    };
-    // waves 4-7: the previous step's tile (its dSᵀ half and sums are still in place)
-    auto late_tile = [&](int lq, bool signal) {
-        f32x16 acc;
-        dq_mfma(acc, lq);
-        if (signal && lq == 0) __hip_atomic_fetch_add(&s_dq, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        vm_wait<0>();
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) reg_fence(lpin[c4]);
-        dq_finish(acc, lpin, lt_t, lt_pofs, lt_ldpin, lt_direct, lt_final, lt_plain, lq);
-    };
-
     bool pub_prev = false;   // the last step left a publish for lane 0 (kind in s_hc.pub)
     for (int i = 0; i < NS; ++i) {
         t = cur.t;
@@ -1494,23 +1380,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // is published after B2.  (vmcnt retires in issue order; a poll load behind
         // those stores would wait for them, hence the poll's place.)
         const bool has_tile = NTQ >= 8 || wave < NTQ;
-        if (!kStag && has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
-        else __builtin_amdgcn_s_waitcnt(0x0F70);                                              // vmcnt(0)
+        if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
         if (i == 0 && tid == 0 && !(abl & 1)) {
             if (pos > 0) poll(lk.ch, t, pos);
             if (btail) s_direct[0] = !hc()->nodirect && ld_agent(hc()->fin + t) >= 1u ? 1u : 0u;
         }
         __syncthreads();
-        unsigned sdword = 0u, slword = 0u;   // (kStag) this slice's direct / local words, stable from B1 on
-        if constexpr (kStag) {
-            sdword = btail ? s_direct[i & 1] : 0u;
-            slword = s_local;
-            if (late && i > 0) late_tile(lq, true);
-            // dead until after B2 on every path (else they would be live across phase A)
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) lpin[c4] = u32x4{0u, 0u, 0u, 0u};
-            lt_pofs = 0;
-        }
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
         const int pofs = lk.ch * pchain4 + (t * NTQ + wave) * 4096 + lq * 16;
@@ -1549,15 +1425,9 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) dk[cb] = mfma32x32x16(rowfrag(qimg, cb, u, s2), dsf[s2], dk[cb]);
             // dSᵀ row kj: queries 32u + 16 s2 + 8h + {0..7}
-            if (kStag && u == 1 && i > 0) {   // the late tiles have read the last slice's u = 1 half
-                while (__hip_atomic_load(&s_dq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * (unsigned)i)
-                    __builtin_amdgcn_s_sleep(1);
-            }
 #pragma unroll
             for (int s2 = 0; s2 < 2 && !(abl & 32); ++s2)
                 *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow)) * 16)) = dsf[s2];
-            if (kStag && u == 0 && lane == 0)
-                __hip_atomic_fetch_add(&s_u0, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
 
         // running sum of the members before this one (sc1 loads, after B1).  Loaded
@@ -1581,29 +1451,11 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 if (bt) s_direct[(i + 1) & 1] = !hc()->nodirect && (f0 >= 1u || ld_agent(fw) >= 1u) ? 1u : 0u;
             }
         }
-        if (kStag && !late) {
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4)
-                pin[c4] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, pofs + c4 * 1024, 0, 16));
-        } else if (has_tile && !late && !(abl & 10)) {
+        if (has_tile && !(abl & 10)) {
             pin[0] = load16_sc1_asm<0>(pdesc, pofs);
             pin[1] = load16_sc1_asm<1024>(pdesc, pofs);
             pin[2] = load16_sc1_asm<2048>(pdesc, pofs);
             pin[3] = load16_sc1_asm<3072>(pdesc, pofs);
-        }
-        if constexpr (kStag) {
-            if (!late) {   // waves 0-3: this slice's tile, once every wave's u = 0 dSᵀ rows are in
-                const bool direct_ = btail && __builtin_amdgcn_readfirstlane(sdword) != 0u;
-                const bool local_ = __builtin_amdgcn_readfirstlane(slword) != 0u;
-                while (__hip_atomic_load(&s_u0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 8u * (unsigned)(i + 1))
-                    __builtin_amdgcn_s_sleep(1);
-                f32x16 acc;
-                dq_mfma(acc, lq);
-                vm_wait<0>();
-#pragma unroll
-                for (int c4 = 0; c4 < 4; ++c4) reg_fence(pin[c4]);
-                dq_finish(acc, pin, t, pofs, ldpin, direct_, (tail && !lk.wrap) || direct_, local_ && !tail, lq);
-            }
         }
         // a chain-B tail at d, dv <= 64 loads chain A's total here too, before it knows
         // (after B2) whether A had finished at its poll: used only if it had (then the
@@ -1623,27 +1475,12 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         // chain B's tail: whether A's total was there at the poll (lane 0's word, ordered
         // by B2).  Read and waited for here: the dQ phase below counts its own LDS reads
         // by hand (lgkm_wait), so no compiler-issued LDS read may land among them.
-        const unsigned dword = kStag ? sdword : btail ? s_direct[i & 1] : 0u;
-        const unsigned lword = kStag ? slword : s_local;
+        const unsigned dword = btail ? s_direct[i & 1] : 0u;
+        const unsigned lword = s_local;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const bool direct = btail && __builtin_amdgcn_readfirstlane(dword) != 0u;
         const bool local = __builtin_amdgcn_readfirstlane(lword) != 0u;
         if (pub_prev && tid == 0) publish((unsigned)i);
-        if constexpr (kStag) {
-            if (late) {   // this slice's tile runs at the start of the next step
-                lt_t = t;
-                lt_pofs = pofs;
-                lt_ldpin = ldpin;
-                lt_direct = direct;
-                lt_final = (tail && !lk.wrap) || direct;
-                lt_plain = local && !tail;
-                // compiler-visible loads (sc1): live across the loop's back edge, where the
-                // compiler may copy them; it waits for them before any such copy
-#pragma unroll
-                for (int c4 = 0; c4 < 4; ++c4)
-                    lpin[c4] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, pofs + c4 * 1024, 0, 16));
-            }
-        }
 
         // next slice's images and row constants (land before the next B1)
         // (the last step reloads its own slice: harmless, nothing reads it)
@@ -1660,15 +1497,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             }
         }
 
-        if constexpr (kStag) {
-            if (tq < 128) {   // the next slice's row constants (phase A's reads of rowc ended at B2)
-                vm_wait<NDMA>();
-                reg_fence(rc);
-                lds_w32(rowc + tq, rc_in ? rc : (tq < 64 ? kNegInf : 0.0f));
-            }
-        }
         // ---- dQᵀ tile (features 32 cbq.., queries 32 uq..) over the 256 keys ----
-        if (!kStag && has_tile) {
+        if (has_tile) {
             f32x16 acc;
 #pragma unroll
             for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
@@ -1763,9 +1593,6 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
         pub_prev = kind != 0u;
         if (tid == 0) hc()->pub = kind | (unsigned)lk.ch << 2 | (unsigned)pos << 3 | (unsigned)t << 12;
         cur = nxt;
-    }
-    if constexpr (kStag) {
-        if (late && NS > 0) late_tile(opaque(tid) & 63, false);
     }
     if (pub_prev) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
