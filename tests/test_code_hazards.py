@@ -79,3 +79,34 @@ def test_disassembly_leaves_the_library_untouched():
     H.disassemble(LIB)
     after = os.stat(LIB)
     assert (before.st_mtime_ns, before.st_ino, before.st_size) == (after.st_mtime_ns, after.st_ino, after.st_size)
+
+
+def test_asm_sum_loads_are_not_read_before_their_wait():
+    # the compiler does not know the asm loads are in flight: a copy of their destination
+    # registers before the kernel's vmcnt wait would take the old contents (a round-6
+    # experiment that carried such loads across the loop's back edge got wrong dQ)
+    import vmem_sgpr_hazards as H
+    if not os.path.exists(LIB):
+        pytest.skip("libfa_hip.so not built")
+    if shutil.which("objcopy") is None or not os.path.exists(os.path.join(H.LLVM, "llvm-objdump")):
+        pytest.skip("binutils / ROCm llvm tools missing")
+    lines = H.disassemble(LIB)
+    assert sum(1 for l in lines if H.ASM_LOAD.match(l.strip().split("//")[0].strip())) >= 18, \
+        "bwd_fused's asm sum loads were not found"
+    found = H.scan_asm_loads(lines)
+    assert not found, "\n".join(f"{f}: {a} -> {b}" for f, a, b in found[:10])
+
+
+def test_asm_load_checker_sees_early_reads():
+    import vmem_sgpr_hazards as H
+    body = ["0000000000001000 <_ZN2fa9bwd_fusedE>:",
+            "\tbuffer_load_dwordx4 v[4:7], v2, s[0:3], 0 offen sc1",
+            "\tv_mfma_f32_32x32x16_bf16 v[8:23], v[0:3], v[24:27], v[8:23]",
+            "\tv_mov_b32_e32 v30, v5",
+            "\ts_waitcnt vmcnt(0)"]
+    found = H.scan_asm_loads(body)
+    assert len(found) == 1 and found[0][2].startswith("v_mov_b32_e32 v30, v5")
+    ok = body[:3] + ["\ts_waitcnt vmcnt(0)", "\tv_mov_b32_e32 v30, v5"]
+    assert not H.scan_asm_loads(ok)
+    clobber = body[:2] + ["\tv_mov_b32_e32 v6, 0", "\ts_waitcnt vmcnt(0)"]
+    assert len(H.scan_asm_loads(clobber)) == 1

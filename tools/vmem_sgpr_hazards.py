@@ -18,6 +18,9 @@ into a scratch output file.  (Without the output operand objcopy rewrites its in
 in place, which truncates the file under any process that has it mapped: the kernel
 then drops that process's relocated private pages and its next C++ unwind faults.)
 
+A second check (scan_asm_loads): the destination registers of bwd_fused's asm
+running-sum loads are not read, copied or overwritten before a vmcnt wait.
+
 Usage: python tools/vmem_sgpr_hazards.py [libfa_hip.so]   (exit 1 if any is found)"""
 import os
 import re
@@ -141,14 +144,65 @@ def scan(lines):
     return found
 
 
+VGPR = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+ASM_LOAD = re.compile(r"^buffer_load_dwordx4 (v\[\d+:\d+\]), .*\bsc1\b")
+STORE = re.compile(r"^(buffer_store|global_store|ds_write|scratch_store|flat_store)")
+
+
+def vregs(text):
+    r = set()
+    for m in VGPR.finditer(text):
+        if m.group(3) is not None:
+            r.add(int(m.group(3)))
+        else:
+            r.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return r
+
+
+def scan_asm_loads(lines, func_filter="bwd_fused"):
+    """The asm running-sum loads of bwd_fused (`buffer_load_dwordx4 ... sc1`, issued by
+    load16_sc1_asm) are hidden from the compiler's waitcnt model: it treats their
+    destination registers as written at issue.  A copy, read or overwrite of those
+    registers before the kernel's own `s_waitcnt vmcnt` would see the old contents.
+    Walks the fall-through path from each such load to the first vmcnt wait (or branch);
+    returns [(function, load, offending instruction)]."""
+    found = []
+    for func, ins, _labels in _functions(lines):
+        if func_filter not in func:
+            continue
+        for i, t in enumerate(ins):
+            m = ASM_LOAD.match(t)
+            if not m:
+                continue
+            dst = vregs(m.group(1))
+            for u in ins[i + 1:]:
+                if (u.startswith("s_waitcnt") and "vmcnt" in u) or u.startswith(("s_branch", "s_cbranch", "s_endpgm")):
+                    break
+                op, _, rest = u.partition(" ")
+                if STORE.match(op):
+                    srcs, dsts = vregs(rest), set()
+                else:
+                    first, _, others = rest.partition(",")
+                    srcs, dsts = vregs(others), (set() if op.startswith("buffer_load") else vregs(first))
+                if (srcs | dsts) & dst:
+                    found.append((func, t, u))
+                    break
+    return found
+
+
 def main():
     lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "flashattention.jl_amd", "libfa_hip.so")
-    found = scan(disassemble(lib))
+    lines = disassemble(lib)
+    found = scan(lines)
     for f, a, b, ws in found:
         print(f"{f}: {a}  ->  {b}  ({ws} wait states)")
     print(f"{len(found)} VALU-SGPR -> VMEM hazards")
-    return 1 if found else 0
+    early = scan_asm_loads(lines)
+    for f, a, b in early:
+        print(f"{f}: {a}  ->  {b}  (before its vmcnt wait)")
+    print(f"{len(early)} asm-load results touched before their wait")
+    return 1 if found or early else 0
 
 
 if __name__ == "__main__":
