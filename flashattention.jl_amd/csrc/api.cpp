@@ -172,16 +172,6 @@ int fa_debug_set_bwd_xcd(int v) {
     return old;
 }
 
-// Not part of the public header: the single-pass backward's waves per workgroup at
-// d = dv = 128 (8: two waves per SIMD, 32 keys each; 4: one wave per SIMD, 64 keys
-// each); returns the previous value (-2 for an invalid argument).
-int fa_debug_set_bwd_waves(int v) {
-    const int old = fa::g_bwd_waves;
-    if (v != 4 && v != 8) return -2;
-    fa::g_bwd_waves = v;
-    return old;
-}
-
 // Not part of the public header: the single-pass backward's step offset between
 // consecutive members of a slice's chain (1..4, default 3); returns the previous value
 // (-2 for an invalid argument).

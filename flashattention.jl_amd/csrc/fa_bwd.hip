@@ -954,14 +954,14 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_fast(BwdParams p) {
 // gives rows 0 and 4 the same slot: measured 6.7e7 conflict cycles at N = 8192.)
 __device__ __forceinline__ int swzds(int f) { return ((f >> 3) & 1) | ((f & 1) << 1) | (((f >> 1) & 1) << 2); }
 
-// [R rows][64 tokens] LDS image written by NW waves (cf. dma_image).
-template <int R, int NW = 8>
+// [R rows][64 tokens] LDS image written by 8 waves (cf. dma_image).
+template <int R>
 __device__ __forceinline__ void dma_image8(__amdgpu_buffer_rsrc_t rs, char* img, int ntok, int t0, int wave, int lane) {
     constexpr int NB = R / 8;                          // 1-KiB blocks
 #pragma unroll
-    for (int it = 0; it < (NB + NW - 1) / NW; ++it) {
-        const int blk = it * NW + wave;
-        if (NB % NW == 0 || blk < NB) {
+    for (int it = 0; it < (NB + 7) / 8; ++it) {
+        const int blk = it * 8 + wave;
+        if (NB % 8 == 0 || blk < NB) {
             const int P = blk * 64 + lane;
             const int f = P >> 3, c = (P & 7) ^ swz16(f);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -1079,14 +1079,14 @@ __device__ __forceinline__ u32x4 load16_sc1_asm(const u32x4& desc, int voff) {
     asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 sc1" : "=v"(r) : "v"(voff), "s"(desc), "i"(OFF) : "memory");
     return r;
 }
-// dma_image8 through dma16_asm; returns nothing, issues (R/8 + NW - 1)/NW ops or fewer per wave
-template <int R, int NW = 8>
+// dma_image8 through dma16_asm; returns nothing, issues (R/8 + 7)/8 ops or fewer per wave
+template <int R>
 __device__ __forceinline__ void dma_image8_asm(const u32x4& desc, char* img, int ntok, int t0, int wave, int lane) {
     constexpr int NB = R / 8;
 #pragma unroll
-    for (int it = 0; it < (NB + NW - 1) / NW; ++it) {
-        const int blk = it * NW + wave;
-        if (NB % NW == 0 || blk < NB) {
+    for (int it = 0; it < (NB + 7) / 8; ++it) {
+        const int blk = it * 8 + wave;
+        if (NB % 8 == 0 || blk < NB) {
             const int P = blk * 64 + lane;
             const int f = P >> 3, c = (P & 7) ^ swz16(f);
             dma16_asm(desc, lds_addr(img + blk * 1024), (f * ntok + t0 + 8 * c) * 2);
@@ -1105,75 +1105,15 @@ __device__ __forceinline__ void vm_wait() {
     __builtin_amdgcn_s_waitcnt(0x0F70 | N);
 }
 
-// acc += A·B with the accumulator pinned in AGPRs (the one-wave-per-SIMD kernel's dKᵀ / dVᵀ).
-// s_nop 1: two wait states after a VALU write of the B operand (the hazard recognizer
-// does not see into asm); back-to-back accumulation into the same AGPRs needs none.
-__device__ __forceinline__ void mfma_agpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma_agpr(f32x16& acc, const f16x8& a, const f16x8& b) {
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-// >= 18 wait states after the last asm MFMA before anything else touches its accumulator
-__device__ __forceinline__ void mfma_agpr_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
-// Diagnostic phase stamps (tools/exp/bwd4_stamp.py; empty in the product build):
-// -DFA_BWD_STAMP4=w records s_memtime of workgroup w's first lane at phase points of
-// its first 128 steps.
-#ifdef FA_BWD_STAMP4
-__device__ unsigned long long g_bwd_stamp[128 * 16];
-#define BWD_STAMP(pt)                                                                          \
-    do {                                                                                       \
-        __builtin_amdgcn_sched_barrier(0);                                                     \
-        if (blockIdx.x == FA_BWD_STAMP4 && threadIdx.x == 0 && i < 128)                        \
-            g_bwd_stamp[i * 16 + (pt)] = __builtin_amdgcn_s_memtime();                         \
-        __builtin_amdgcn_sched_barrier(0);                                                     \
-    } while (0)
-#else
-#define BWD_STAMP(pt)
-#endif
-#ifndef FA_BWD_ABL4
-#define FA_BWD_ABL4 0   // timing-only ablations of the one-wave phase A (stamped builds; WRONG results)
-#endif
-#ifndef FA_BWD_FG4
-#define FA_BWD_FG4 2   // one-wave phase A: MFMA slots per sched_barrier-fenced region
-#endif
-#ifndef FA_BWD_DQPF
-#define FA_BWD_DQPF 3  // one-wave dQ phase: LDS operand reads this many k-steps ahead
-#endif
-#ifndef FA_BWD_PF4
-#define FA_BWD_PF4 2
-#endif
-#ifndef FA_BWD_PA4
-#define FA_BWD_PA4 3
-#endif
-// acc += A·B with a VGPR accumulator (the hand-ordered phase A); FIRST: the chain's first
-// product, whose C was just written by VALU (two wait states)
-template <bool FIRST>
-__device__ __forceinline__ void mfma_vgpr(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-    if constexpr (FIRST) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-    else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-template <bool FIRST>
-__device__ __forceinline__ void mfma_vgpr(f32x16& acc, const f16x8& a, const f16x8& b) {
-    if constexpr (FIRST) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-    else asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-
-template <class T, int D, int DV, int NW = 8>
-__global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
+template <class T, int D, int DV>
+__global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     typedef typename Frag8<T>::type F8;
     typedef typename Frag8<T>::half F4;
     constexpr int KSUB = D * 128;                  // K image of 64 keys: [D][64]
     constexpr int QB = D * 128, OB = DV * 128;
     constexpr int STAGE = QB + OB + 512;           // Q, dO images + (−lse, −D) of one slice
     constexpr int DSB = 256 * 128;                 // dSᵀ image [256 keys][64 queries]
-    constexpr int NTQ = D / 16;                    // 32 x 32 dQᵀ tiles per slice
-    // NW waves of KPW keys: 8 x 32 (two waves per SIMD) or 4 x 64 (one wave per SIMD;
-    // each Q / dO fragment it reads from LDS feeds its NKB key blocks)
-    static_assert(NW == 8 || NW == 4, "waves per workgroup");
-    constexpr int KPW = 256 / NW, NKB = KPW / 32;
-    constexpr int TPW = NTQ >= NW ? NTQ / NW : 1;  // dQᵀ tiles per wave
-    static_assert(TPW == 1 || NW % (D / 32) == 0, "a wave's dQ tiles share their K rows");
+    constexpr int NTQ = D / 16;                    // 32 x 32 dQᵀ tiles per slice (<= 8 waves)
     __shared__ __attribute__((aligned(16))) char smem[4 * KSUB + STAGE + DSB];
     char* const kimg = smem;
     char* const qimg = smem + 4 * KSUB;
@@ -1197,13 +1137,8 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
     const auto krs = bslab<T>(p.K, (int64_t)b * Nk * D, (int64_t)Nk * D);
     const auto vrs = bslab<T>(p.V, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
     const int key0 = j * 256;
-    int kj[NKB];   // this lane's keys (columns of S, dP, dKᵀ, dVᵀ), one per key block
-    bool key_ok[NKB];
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-        kj[kb] = key0 + KPW * wave + 32 * kb + sig32(r);
-        key_ok[kb] = kj[kb] < Nk;
-    }
+    const int kj = key0 + 32 * wave + sig32(r);   // this lane's key (column of S, dP, dKᵀ, dVᵀ)
+    const bool key_ok = kj < Nk;
     const float c = p.scale_log2;
     const float* nlse = p.nlse + (int64_t)b * N;
     const float* nDg = p.nD + (int64_t)b * N;
@@ -1215,7 +1150,7 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
     const u32x4 qdesc = desc_of((const T*)p.Q + (int64_t)b * N * D, (uint32_t)(N * D * 2));
     const u32x4 odesc = desc_of((const T*)p.dO + (int64_t)b * N * DV, (uint32_t)(N * DV * 2));
     // this wave's loop DMA ops per slice (dma_image8_asm), >= for every wave: a lower bound
-    constexpr int NDMA = (D / 8) / NW + (DV / 8) / NW;
+    constexpr int NDMA = (D / 8 >= 8 ? D / 64 : 0) + (DV / 8 >= 8 ? DV / 64 : 0);
     // The hand-off's bookkeeping (polls, publishes, the XCD words) is lane 0's alone, so
     // its pointers and state live in LDS, read where they are used through an address
     // the compiler cannot see through (hc(): never hoisted into registers).  Held in
@@ -1376,48 +1311,32 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
     {
         const float rc = load_rowc(t);
 #pragma unroll
-        for (int i4 = 0; i4 < 4; ++i4) dma_image8<D, NW>(krs, kimg + i4 * KSUB, Nk, key0 + 64 * i4, wave, lane);
-        dma_image8<D, NW>(qrs, qimg, N, t * 64, wave, lane);
-        dma_image8<DV, NW>(ors, oimg, N, t * 64, wave, lane);
+        for (int i4 = 0; i4 < 4; ++i4) dma_image8<D>(krs, kimg + i4 * KSUB, Nk, key0 + 64 * i4, wave, lane);
+        dma_image8<D>(qrs, qimg, N, t * 64, wave, lane);
+        dma_image8<DV>(ors, oimg, N, t * 64, wave, lane);
         if (tid < 128) rowc[tid] = rc;
     }
-    F8 vf[NKB][DV / 16];
+    F8 vf[DV / 16];
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
+    for (int s = 0; s < DV / 16; ++s)
 #pragma unroll
-        for (int s = 0; s < DV / 16; ++s)
+        for (int e = 0; e < 8; ++e) {
+            const T x = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(vrs, ((16 * s + 8 * h + e) * Nk + kj) * 2, 0, 0));
+            vf[s][e] = key_ok ? x : (T)0.0f;
+        }
+    f32x16 dk[D / 32], dv[DV / 32];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const T x = __builtin_bit_cast(
-                    T, __builtin_amdgcn_raw_buffer_load_b16(vrs, ((16 * s + 8 * h + e) * Nk + kj[kb]) * 2, 0, 0));
-                vf[kb][s][e] = key_ok[kb] ? x : (T)0.0f;
-            }
-    f32x16 dk[NKB][D / 32], dv[NKB][DV / 32];
+    for (int cb = 0; cb < D / 32; ++cb)
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
+        for (int x = 0; x < 16; ++x) dk[cb][x] = 0.0f;
 #pragma unroll
-        for (int cb = 0; cb < D / 32; ++cb)
+    for (int cb = 0; cb < DV / 32; ++cb)
 #pragma unroll
-            for (int x = 0; x < 16; ++x) dk[kb][cb][x] = 0.0f;
-#pragma unroll
-        for (int cb = 0; cb < DV / 32; ++cb)
-#pragma unroll
-            for (int x = 0; x < 16; ++x) dv[kb][cb][x] = 0.0f;
-    }
-    if constexpr (NW == 4) mfma_agpr_drain();   // the zeroed AGPRs before the first asm MFMA reads them
-    const char* kmine[NKB];   // the 64-key image holding key block kb, and its 32-key half
-    int ktb[NKB], dsrow[NKB];  // ... and this lane's dSᵀ row
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-        kmine[kb] = kimg + ((NKB * wave + kb) >> 1) * KSUB;
-        ktb[kb] = (NKB * wave + kb) & 1;
-        dsrow[kb] = KPW * wave + 32 * kb + sig32(r);
-    }
-    // this wave's dQᵀ tiles wave + NW·ti (wave < NTQ): features 32 cbq.., queries 32 uq[ti]..
-    const int cbq = wave % (D / 32);
-    int uq[TPW];
-#pragma unroll
-    for (int ti = 0; ti < TPW; ++ti) uq[ti] = (wave + NW * ti) / (D / 32);
+        for (int x = 0; x < 16; ++x) dv[cb][x] = 0.0f;
+    const char* const kmine = kimg + (wave >> 1) * KSUB;   // the 64-key image holding this wave's keys
+    const int ktb = wave & 1;
+    const int dsrow = 32 * wave + sig32(r);                  // this lane's dSᵀ row
+    const int cbq = wave % (D / 32), uq = wave / (D / 32);   // this wave's dQᵀ tile (wave < NTQ)
 
     // the prologue's loads have landed: no LDS-DMA the compiler knows of is pending in
     // the loop (its DMA is asm), so it adds no vmcnt(0) before the loop's LDS reads
@@ -1460,205 +1379,57 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
         // be in flight: every wave drains them in the middle of phase A and their count
         // is published after B2.  (vmcnt retires in issue order; a poll load behind
         // those stores would wait for them, hence the poll's place.)
-        const bool has_tile = NTQ >= NW || wave < NTQ;
-        if (has_tile && i > 0 && !(abl & 18)) vm_wait<4 * TPW>();
-        else vm_wait<0>();
+        const bool has_tile = NTQ >= 8 || wave < NTQ;
+        if (has_tile && i > 0 && !(abl & 18)) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                                    // vmcnt(0)
         if (i == 0 && tid == 0 && !(abl & 1)) {
             if (pos > 0) poll(lk.ch, t, pos);
             if (btail) s_direct[0] = !hc()->nodirect && ld_agent(hc()->fin + t) >= 1u ? 1u : 0u;
         }
         __syncthreads();
-#ifdef FA_BWD_STAGGER_SLEEP
-        if (wave >= 4) __builtin_amdgcn_s_sleep(FA_BWD_STAGGER_SLEEP);   // timing experiment: waves 4-7 start late
-#endif
-        BWD_STAMP(0);
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
-        int pofs[TPW];
-#pragma unroll
-        for (int ti = 0; ti < TPW; ++ti) pofs[ti] = lk.ch * pchain4 + (t * NTQ + wave + NW * ti) * 4096 + lq * 16;
+        const int pofs = lk.ch * pchain4 + (t * NTQ + wave) * 4096 + lq * 16;
         const bool ldpin = pos > 0 && has_tile && !(abl & 10);
-        u32x4 pin[TPW][4];
-        if constexpr (NW == 4) {
-            // One wave per SIMD, hand-ordered: units n = 2u + kb (query half u, key block
-            // kb), two in flight.  Each group of 16 asm MFMAs carries the VALU of the unit
-            // before it (S / dP of unit n + 1 under the softmax / dS of unit n), or dV / dK
-            // of a unit under the dSᵀ writes; sched_barrier(0) fences every slot.
-            static_assert(D == 128 && DV == 128, "hand-ordered phase A: d = dv = 128");
-            f32x16 sacc[2], dacc[2];
-            F8 pfr[2][2], dsr[2][2];
-            auto fence = []() { __builtin_amdgcn_sched_barrier(0); };
-            auto init_unit = [&](auto nc) {
-                constexpr int n = decltype(nc)::value, u = n >> 1, m = n & 1;
-                const f32x4* Lq = (const f32x4*)(rowc + u * 32 + 8 * h);
-                const f32x4* Dq = (const f32x4*)(rowc + 64 + u * 32 + 8 * h);
-                const f32x4 l0 = Lq[0], l1 = Lq[1], l2 = Lq[4], l3 = Lq[5];
-                const f32x4 d0 = Dq[0], d1 = Dq[1], d2 = Dq[4], d3 = Dq[5];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    sacc[m][e] = l0[e]; sacc[m][4 + e] = l1[e]; sacc[m][8 + e] = l2[e]; sacc[m][12 + e] = l3[e];
-                    dacc[m][e] = d0[e]; dacc[m][4 + e] = d1[e]; dacc[m][8 + e] = d2[e]; dacc[m][12 + e] = d3[e];
-                }
-            };
-            // element x of unit n: P and dS (about five VALU instructions)
-            auto valu = [&](auto nc, int x) {
-                constexpr int kb = decltype(nc)::value & 1, m = kb;
-                const float pr = key_ok[kb] ? exp2_fast(sacc[m][x] * c) : 0.0f;
-                pfr[m][x >> 3][x & 7] = (T)pr;
-                dsr[m][x >> 3][x & 7] = (T)(pr * dacc[m][x]);
-            };
-            auto ds_out = [&](auto nc, int s2) {   // dSᵀ row of key block kb: queries 32u + 16 s2 + 8h + {0..7}
-                constexpr int n = decltype(nc)::value, u = n >> 1, kb = n & 1, m = kb;
-                *(F8*)(dsimg + dsrow[kb] * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow[kb])) * 16)) = dsr[m][s2];
-            };
-            // LDS operands run FA_BWD_PF4 s-steps (2 MFMAs each) ahead of their MFMAs
-            constexpr int PF = FA_BWD_PF4;
-            auto sdp_group = [&](auto nc, auto&& fill) {   // S and dP of unit n (16 MFMAs)
-                constexpr int n = decltype(nc)::value, u = n >> 1, kb = n & 1, m = kb;
-                F8 qf[PF + 1], kf[PF + 1], of[PF + 1];
-                static_for<PF>([&](auto pc) {
-                    constexpr int s_ = decltype(pc)::value;
-                    qf[s_] = trfrag(qimg, u, s_);
-                    kf[s_] = trfrag(kmine[kb], ktb[kb], s_);
-                    of[s_] = trfrag(oimg, u, s_);
-                });
-                static_for<8>([&](auto sc) {
-                    constexpr int s_ = decltype(sc)::value, r_ = s_ % (PF + 1);
-                    if constexpr (s_ + PF < 8) {
-                        constexpr int w_ = (s_ + PF) % (PF + 1);
-                        qf[w_] = trfrag(qimg, u, s_ + PF);
-                        kf[w_] = trfrag(kmine[kb], ktb[kb], s_ + PF);
-                        of[w_] = trfrag(oimg, u, s_ + PF);
-                    }
-                    mfma_vgpr<s_ == 0>(sacc[m], qf[r_], kf[r_]);
-                    if constexpr (!(FA_BWD_ABL4 & 2)) fill(2 * s_);
-                    if constexpr ((2 * s_ + 1) % FA_BWD_FG4 == 0) fence();
-                    mfma_vgpr<s_ == 0>(dacc[m], of[r_], vf[kb][s_]);
-                    if constexpr (!(FA_BWD_ABL4 & 2)) fill(2 * s_ + 1);
-                    if constexpr ((2 * s_ + 2) % FA_BWD_FG4 == 0) fence();
-                });
-            };
-            auto a_group = [&](auto nc, auto&& fill) {   // dVᵀ, dKᵀ of unit n (16 MFMAs into AGPRs)
-                constexpr int n = decltype(nc)::value, u = n >> 1, kb = n & 1, m = kb;
-                constexpr int PA = FA_BWD_PA4;   // row fragments run PA MFMAs ahead
-                F8 rf[PA + 1];
-                static_for<PA>([&](auto pc) {
-                    constexpr int i1 = decltype(pc)::value;
-                    rf[i1] = rowfrag(i1 >= 8 ? qimg : oimg, (i1 & 7) >> 1, u, i1 & 1);
-                });
-                static_for<16>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value, cb = (i & 7) >> 1, s2 = i & 1, r_ = i % (PA + 1);
-                    if constexpr (i + PA < 16 && !(FA_BWD_ABL4 & 1)) {
-                        constexpr int i1 = i + PA;
-                        rf[i1 % (PA + 1)] = rowfrag(i1 >= 8 ? qimg : oimg, (i1 & 7) >> 1, u, i1 & 1);
-                    }
-                    constexpr int ra = (FA_BWD_ABL4 & 1) ? 0 : r_;
-                    // bit 4: consecutive MFMAs on different accumulators (s2 outer)
-                    constexpr int cbx = (FA_BWD_ABL4 & 4) ? (i & 3) : cb, s2x = (FA_BWD_ABL4 & 4) ? ((i >> 2) & 1) : s2;
-                    if constexpr (i < 8) mfma_agpr(dv[kb][cbx], rf[ra], pfr[m][s2x]);
-                    else mfma_agpr(dk[kb][cbx], rf[ra], dsr[m][s2x]);
-                    fill(i);
-                    if constexpr ((i + 1) % FA_BWD_FG4 == 0) fence();
-                });
-            };
-            using I0 = std::integral_constant<int, 0>;
-            using I1 = std::integral_constant<int, 1>;
-            using I2 = std::integral_constant<int, 2>;
-            using I3 = std::integral_constant<int, 3>;
-            auto none = [](int) {};
-            init_unit(I0{});
-            sdp_group(I0{}, none);
-            BWD_STAMP(1);
-            mfma_agpr_drain();
-            init_unit(I1{});
-            sdp_group(I1{}, [&](int x) { valu(I0{}, x); });
-            BWD_STAMP(2);
-            a_group(I0{}, [&](int x) { if (x < 2) ds_out(I0{}, x); });
-            BWD_STAMP(3);
-            vm_wait<0>();   // last step's sums stored
-            mfma_agpr_drain();
-            init_unit(I2{});
-            sdp_group(I2{}, [&](int x) { valu(I1{}, x); });
-            BWD_STAMP(4);
-            a_group(I1{}, [&](int x) { if (x < 2) ds_out(I1{}, x); });
-            BWD_STAMP(5);
-            mfma_agpr_drain();
-            init_unit(I3{});
-            sdp_group(I3{}, [&](int x) { valu(I2{}, x); });
-            BWD_STAMP(6);
-            mfma_agpr_drain();
-            a_group(I2{}, [&](int x) { valu(I3{}, x); if (x < 2) ds_out(I2{}, x); });
-            BWD_STAMP(7);
-            a_group(I3{}, [&](int x) { if (x < 2) ds_out(I3{}, x); });
-        } else {
+        u32x4 pin[4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            f32x16 sa[NKB], dp[NKB];
+            f32x16 sa, dp;
             const f32x4* Lq = (const f32x4*)(rowc + u * 32 + 8 * h);
             const f32x4* Dq = (const f32x4*)(rowc + 64 + u * 32 + 8 * h);
             const f32x4 l0 = Lq[0], l1 = Lq[1], l2 = Lq[4], l3 = Lq[5];
             const f32x4 d0 = Dq[0], d1 = Dq[1], d2 = Dq[4], d3 = Dq[5];
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    sa[kb][e] = l0[e]; sa[kb][4 + e] = l1[e]; sa[kb][8 + e] = l2[e]; sa[kb][12 + e] = l3[e];
-                    dp[kb][e] = d0[e]; dp[kb][4 + e] = d1[e]; dp[kb][8 + e] = d2[e]; dp[kb][12 + e] = d3[e];
-                }
-#pragma unroll
-            for (int s = 0; s < D / 16; ++s) {
-                const F8 qf = trfrag(qimg, u, s);
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) sa[kb] = mfma32x32x16(qf, trfrag(kmine[kb], ktb[kb], s), sa[kb]);
+            for (int e = 0; e < 4; ++e) {
+                sa[e] = l0[e]; sa[4 + e] = l1[e]; sa[8 + e] = l2[e]; sa[12 + e] = l3[e];
+                dp[e] = d0[e]; dp[4 + e] = d1[e]; dp[8 + e] = d2[e]; dp[12 + e] = d3[e];
             }
 #pragma unroll
-            for (int s = 0; s < DV / 16; ++s) {
-                const F8 of = trfrag(oimg, u, s);
+            for (int s = 0; s < D / 16; ++s) sa = mfma32x32x16(trfrag(qimg, u, s), trfrag(kmine, ktb, s), sa);
 #pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) dp[kb] = mfma32x32x16(of, vf[kb][s], dp[kb]);
+            for (int s = 0; s < DV / 16; ++s) dp = mfma32x32x16(trfrag(oimg, u, s), vf[s], dp);
+            if (u == 1) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): last step's sums stored
+            F8 pf[2], dsf[2];
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                const float pr = key_ok ? exp2_fast(sa[x] * c) : 0.0f;
+                pf[x >> 3][x & 7] = (T)pr;
+                dsf[x >> 3][x & 7] = (T)(pr * dp[x]);
             }
-            if (u == 1) vm_wait<0>();   // last step's sums stored
-            F8 pf[NKB][2], dsf[NKB][2];
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) {
-                    const float pr = key_ok[kb] ? exp2_fast(sa[kb][x] * c) : 0.0f;
-                    pf[kb][x >> 3][x & 7] = (T)pr;
-                    dsf[kb][x >> 3][x & 7] = (T)(pr * dp[kb][x]);
-                }
 #pragma unroll
             for (int cb = 0; cb < DV / 32; ++cb)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    const F8 rf = rowfrag(oimg, cb, u, s2);
-#pragma unroll
-                    for (int kb = 0; kb < NKB; ++kb) {
-                        if constexpr (NW == 4) mfma_agpr(dv[kb][cb], rf, pf[kb][s2]);
-                        else dv[kb][cb] = mfma32x32x16(rf, pf[kb][s2], dv[kb][cb]);
-                    }
-                }
+                for (int s2 = 0; s2 < 2; ++s2) dv[cb] = mfma32x32x16(rowfrag(oimg, cb, u, s2), pf[s2], dv[cb]);
 #pragma unroll
             for (int cb = 0; cb < D / 32; ++cb)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    const F8 rf = rowfrag(qimg, cb, u, s2);
-#pragma unroll
-                    for (int kb = 0; kb < NKB; ++kb) {
-                        if constexpr (NW == 4) mfma_agpr(dk[kb][cb], rf, dsf[kb][s2]);
-                        else dk[kb][cb] = mfma32x32x16(rf, dsf[kb][s2], dk[kb][cb]);
-                    }
-                }
+                for (int s2 = 0; s2 < 2; ++s2) dk[cb] = mfma32x32x16(rowfrag(qimg, cb, u, s2), dsf[s2], dk[cb]);
             // dSᵀ row kj: queries 32u + 16 s2 + 8h + {0..7}
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-                for (int s2 = 0; s2 < 2 && !(abl & 32); ++s2)
-                    *(F8*)(dsimg + dsrow[kb] * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow[kb])) * 16)) = dsf[kb][s2];
+            for (int s2 = 0; s2 < 2 && !(abl & 32); ++s2)
+                *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow)) * 16)) = dsf[s2];
         }
-        }   // NW == 8
 
-        BWD_STAMP(8);
         // running sum of the members before this one (sc1 loads, after B1).  Loaded
         // whether or not this member is the chain's head (which adds nothing), and the
         // DMA and row constants below are unconditional too: a straight-line step
@@ -1681,13 +1452,10 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
             }
         }
         if (has_tile && !(abl & 10)) {
-#pragma unroll
-            for (int ti = 0; ti < TPW; ++ti) {
-                pin[ti][0] = load16_sc1_asm<0>(pdesc, pofs[ti]);
-                pin[ti][1] = load16_sc1_asm<1024>(pdesc, pofs[ti]);
-                pin[ti][2] = load16_sc1_asm<2048>(pdesc, pofs[ti]);
-                pin[ti][3] = load16_sc1_asm<3072>(pdesc, pofs[ti]);
-            }
+            pin[0] = load16_sc1_asm<0>(pdesc, pofs);
+            pin[1] = load16_sc1_asm<1024>(pdesc, pofs);
+            pin[2] = load16_sc1_asm<2048>(pdesc, pofs);
+            pin[3] = load16_sc1_asm<3072>(pdesc, pofs);
         }
         // a chain-B tail at d, dv <= 64 loads chain A's total here too, before it knows
         // (after B2) whether A had finished at its poll: used only if it had (then the
@@ -1695,19 +1463,15 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
         // and counted with the running sum (vm_wait<NDMA>).  At 128 its 16 registers
         // would spill across the dQ phase: loaded after that phase instead.
         constexpr bool kPrefA = D <= 64 && DV <= 64;
-        u32x4 pa[TPW][4];
+        u32x4 pa[4];
         if (kPrefA && has_tile && btail && !(abl & 10)) {
-#pragma unroll
-            for (int ti = 0; ti < TPW; ++ti) {
-                const int pofa = pofs[ti] - pchain4;
-                pa[ti][0] = load16_sc1_asm<0>(pdesc, pofa);
-                pa[ti][1] = load16_sc1_asm<1024>(pdesc, pofa);
-                pa[ti][2] = load16_sc1_asm<2048>(pdesc, pofa);
-                pa[ti][3] = load16_sc1_asm<3072>(pdesc, pofa);
-            }
+            const int pofa = pofs - pchain4;
+            pa[0] = load16_sc1_asm<0>(pdesc, pofa);
+            pa[1] = load16_sc1_asm<1024>(pdesc, pofa);
+            pa[2] = load16_sc1_asm<2048>(pdesc, pofa);
+            pa[3] = load16_sc1_asm<3072>(pdesc, pofa);
         }
         __syncthreads();   // B2: dSᵀ complete, the slice's images free, last step's sums stored
-        BWD_STAMP(9);
         // chain B's tail: whether A's total was there at the poll (lane 0's word, ordered
         // by B2).  Read and waited for here: the dQ phase below counts its own LDS reads
         // by hand (lgkm_wait), so no compiler-issued LDS read may land among them.
@@ -1728,21 +1492,18 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
             rc = load4_asm((tq < 64 ? nlse : nDg) + (q < N ? q : N - 1));   // asm: counted below
             rc_in = q < N;
             if (!(abl & 64)) {
-                dma_image8_asm<D, NW>(qdesc, qimg, N, tn * 64, wave, lq);
-                dma_image8_asm<DV, NW>(odesc, oimg, N, tn * 64, wave, lq);
+                dma_image8_asm<D>(qdesc, qimg, N, tn * 64, wave, lq);
+                dma_image8_asm<DV>(odesc, oimg, N, tn * 64, wave, lq);
             }
         }
 
-        // ---- dQᵀ tiles (features 32 cbq.., queries 32 uq[ti]..) over the 256 keys ----
+        // ---- dQᵀ tile (features 32 cbq.., queries 32 uq..) over the 256 keys ----
         if (has_tile) {
-            f32x16 acc[TPW];
+            f32x16 acc;
 #pragma unroll
-            for (int ti = 0; ti < TPW; ++ti)
-#pragma unroll
-                for (int x = 0; x < 16; ++x) acc[ti][x] = 0.0f;
+            for (int x = 0; x < 16; ++x) acc[x] = 0.0f;
             // asm LDS reads (see lds_b128_at), one step ahead of the MFMA: the DMA
-            // just issued and the running-sum loads stay in flight meanwhile.  A wave's
-            // tiles share the K rows (fa), read once for all of them.
+            // just issued and the running-sum loads stay in flight meanwhile
             uint32_t ka[4];
             const int rswq = swz16(rq);
 #pragma unroll
@@ -1750,109 +1511,83 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
                 ka[q4] = lds_addr(kimg + (cbq * 32 + rq) * 128 + ((((q4 >> 1) * 4 + 2 * (q4 & 1) + hq) ^ rswq) * 16));
             const int qqq = (lq & 15) >> 2, ppq = lq & 3, khq = (lq >> 4) & 1;
             const int sgq = (ppq == 1) ? 2 : (ppq == 2) ? 1 : ppq;
-            uint32_t da[TPW];
-#pragma unroll
-            for (int ti = 0; ti < TPW; ++ti)
-                da[ti] = lds_addr(dsimg + (8 * hq + qqq) * 128 +
-                                  (((uq[ti] * 4 + khq * 2 + (sgq >> 1)) ^ swzds(8 * hq + qqq)) * 16) + (sgq & 1) * 8);
-            // reads QP k-steps ahead (a ring of QP + 1), counted by hand (lgkmcnt <= 15)
-            constexpr int QP = NW == 4 ? FA_BWD_DQPF : 1, QR = QP + 1, QOPS = 1 + 2 * TPW;
-            static_assert(QP * QOPS <= 15, "lgkmcnt");
-            u32x4 fa[QR];
-            s16x4 flo[QR][TPW], fhi[QR][TPW];
+            const uint32_t da = lds_addr(dsimg + (8 * hq + qqq) * 128 +
+                                         (((uq * 4 + khq * 2 + (sgq >> 1)) ^ swzds(8 * hq + qqq)) * 16) + (sgq & 1) * 8);
+            u32x4 fa[2];
+            s16x4 flo[2], fhi[2];
             auto issue = [&](auto kc) {
-                constexpr int kk = decltype(kc)::value, sl = kk % QR;
-                fa[sl] = lds_b128_at<(kk >> 2) * KSUB>(ka[kk & 3]);
-#pragma unroll
-                for (int ti = 0; ti < TPW; ++ti) {
-                    flo[sl][ti] = lds_tr16_at<2048 * kk>(da[ti]);
-                    fhi[sl][ti] = lds_tr16_at<2048 * kk + 512>(da[ti]);
-                }
+                constexpr int kk = decltype(kc)::value;
+                fa[kk & 1] = lds_b128_at<(kk >> 2) * KSUB>(ka[kk & 3]);
+                flo[kk & 1] = lds_tr16_at<2048 * kk>(da);
+                fhi[kk & 1] = lds_tr16_at<2048 * kk + 512>(da);
             };
-            static_for<QP>([&](auto kc) { issue(kc); });
+            issue(std::integral_constant<int, 0>{});
             static_for<16>([&](auto kc) {
-                constexpr int kk = decltype(kc)::value, sl = kk % QR;
-                if constexpr (kk + QP < 16) issue(std::integral_constant<int, kk + QP>{});
-                lgkm_wait<QOPS * (15 - kk < QP ? 15 - kk : QP)>();
-                reg_fence(fa[sl]);
-#pragma unroll
-                for (int ti = 0; ti < TPW; ++ti) {
-                    reg_fence(flo[sl][ti]);
-                    reg_fence(fhi[sl][ti]);
-                    const F4 lo = __builtin_bit_cast(F4, flo[sl][ti]);
-                    const F4 hi = __builtin_bit_cast(F4, fhi[sl][ti]);
-                    if constexpr (NW == 4)   // asm: no compiler MFMA (it would take AGPR form here)
-                        mfma_vgpr<true>(acc[ti], __builtin_bit_cast(F8, fa[sl]),
-                                        __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-                    else
-                        acc[ti] = mfma32x32x16(__builtin_bit_cast(F8, fa[sl]),
-                                               __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), acc[ti]);
+                constexpr int kk = decltype(kc)::value;
+                if constexpr (kk + 1 < 16) {
+                    issue(std::integral_constant<int, kk + 1>{});
+                    lgkm_wait<3>();
+                } else {
+                    lgkm_wait<0>();
                 }
+                reg_fence(fa[kk & 1]);
+                reg_fence(flo[kk & 1]);
+                reg_fence(fhi[kk & 1]);
+                const F4 lo = __builtin_bit_cast(F4, flo[kk & 1]);
+                const F4 hi = __builtin_bit_cast(F4, fhi[kk & 1]);
+                acc = mfma32x32x16(__builtin_bit_cast(F8, fa[kk & 1]), __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7),
+                                   acc);
             });
-            if constexpr (NW == 4) mfma_agpr_drain();   // the asm MFMAs' acc before VALU reads it
             // the sums (asm loads): all but this wave's NDMA DMA ops retired
             if (!(abl & 64)) vm_wait<NDMA>(); else vm_wait<0>();
 #pragma unroll
-            for (int ti = 0; ti < TPW; ++ti)
-#pragma unroll
-                for (int c4 = 0; c4 < 4; ++c4) reg_fence(pin[ti][c4]);
+            for (int c4 = 0; c4 < 4; ++c4) reg_fence(pin[c4]);
             reg_fence(rc);
             // the next slice's row constants (phase A's reads of rowc ended at B2)
             if (tq < 128) lds_w32(rowc + tq, rc_in ? rc : (tq < 64 ? kNegInf : 0.0f));
             if (ldpin) {
 #pragma unroll
-                for (int ti = 0; ti < TPW; ++ti)
+                for (int c4 = 0; c4 < 4; ++c4)
 #pragma unroll
-                    for (int c4 = 0; c4 < 4; ++c4)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) acc[ti][4 * c4 + e] += __uint_as_float(pin[ti][c4][e]);
+                    for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pin[c4][e]);
             }
             // chain B's tail with A finished: A's total (its tail's sc1 stores, published
             // through fin before this step's poll) in, after this chain's own sum
             if (direct) {
+                if constexpr (!kPrefA) {
+                    const int pofa = pofs - pchain4;
+                    pa[0] = load16_sc1_asm<0>(pdesc, pofa);
+                    pa[1] = load16_sc1_asm<1024>(pdesc, pofa);
+                    pa[2] = load16_sc1_asm<2048>(pdesc, pofa);
+                    pa[3] = load16_sc1_asm<3072>(pdesc, pofa);
+                    vm_wait<0>();
+                }
 #pragma unroll
-                for (int ti = 0; ti < TPW; ++ti) {
-                    if constexpr (!kPrefA) {
-                        const int pofa = pofs[ti] - pchain4;
-                        pa[ti][0] = load16_sc1_asm<0>(pdesc, pofa);
-                        pa[ti][1] = load16_sc1_asm<1024>(pdesc, pofa);
-                        pa[ti][2] = load16_sc1_asm<2048>(pdesc, pofa);
-                        pa[ti][3] = load16_sc1_asm<3072>(pdesc, pofa);
-                        vm_wait<0>();
-                    }
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    reg_fence(pa[c4]);
 #pragma unroll
-                    for (int c4 = 0; c4 < 4; ++c4) {
-                        reg_fence(pa[ti][c4]);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) acc[ti][4 * c4 + e] += __uint_as_float(pa[ti][c4][e]);
-                    }
+                    for (int e = 0; e < 4; ++e) acc[4 * c4 + e] += __uint_as_float(pa[c4][e]);
                 }
             }
             if ((tail && !lk.wrap) || direct) {
                 // 32-bit lane offset + scalar row offset (no hoisted 64-bit addresses)
+                const int q = t * 64 + 32 * uq + sig32(rq);
                 const auto qo = bslab<T>(p.dQ, (int64_t)b * N * D, (int64_t)N * D);
+                const int vo = q < N ? ((cbq * 32 + 4 * hq) * N + q) * 2 : N * D * 2;   // past N: dropped
 #pragma unroll
-                for (int ti = 0; ti < TPW; ++ti) {
-                    const int q = t * 64 + 32 * uq[ti] + sig32(rq);
-                    const int vo = q < N ? ((cbq * 32 + 4 * hq) * N + q) * 2 : N * D * 2;   // past N: dropped
-#pragma unroll
-                    for (int x = 0; x < 16; ++x)
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[ti][x] * p.scale)),
-                                                              qo, vo, ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
-                }
+                for (int x = 0; x < 16; ++x)
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(acc[x] * p.scale)), qo, vo,
+                                                          ((x & 3) + 8 * (x >> 2)) * N * 2, 0);
             } else if (!(abl & 18)) {
 #pragma unroll
-                for (int ti = 0; ti < TPW; ++ti)
-#pragma unroll
-                    for (int c4 = 0; c4 < 4; ++c4) {
-                        const u32x4 v4 = {__float_as_uint(acc[ti][4 * c4]), __float_as_uint(acc[ti][4 * c4 + 1]),
-                                          __float_as_uint(acc[ti][4 * c4 + 2]), __float_as_uint(acc[ti][4 * c4 + 3])};
-                        if (local && !tail) __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs[ti] + c4 * 1024, 0, 0);
-                        else __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs[ti] + c4 * 1024, 0, 16);   // sc1
-                    }
+                for (int c4 = 0; c4 < 4; ++c4) {
+                    const u32x4 v4 = {__float_as_uint(acc[4 * c4]), __float_as_uint(acc[4 * c4 + 1]),
+                                      __float_as_uint(acc[4 * c4 + 2]), __float_as_uint(acc[4 * c4 + 3])};
+                    if (local && !tail) __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 0);
+                    else __builtin_amdgcn_raw_buffer_store_b128(v4, prs, pofs + c4 * 1024, 0, 16);   // sc1
+                }
             }
         }
-        BWD_STAMP(10);
         // publish kind: 0 none (dQ written), 1 chain count, 2 fin word (a wrapped chain's tail)
         const unsigned kind = (tail && !lk.wrap) || direct ? 0u : tail ? 2u : 1u;
         pub_prev = kind != 0u;
@@ -1864,33 +1599,25 @@ __global__ __launch_bounds__(64 * NW, 1) void bwd_fused(BwdParams p) {
         __syncthreads();
         if (tid == 0) publish((unsigned)NS);
     }
-    if constexpr (NW == 4) mfma_agpr_drain();
-    const auto ko = bslab<T>(p.dK, (int64_t)b * Nk * D, (int64_t)Nk * D);
-    const auto vo = bslab<T>(p.dV, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-        if (!key_ok[kb]) continue;
-        const int lo = (4 * h * Nk + kj[kb]) * 2;
+    if (key_ok) {
+        const auto ko = bslab<T>(p.dK, (int64_t)b * Nk * D, (int64_t)Nk * D);
+        const auto vo = bslab<T>(p.dV, (int64_t)b * Nk * DV, (int64_t)Nk * DV);
+        const int lo = (4 * h * Nk + kj) * 2;
 #pragma unroll
         for (int cb = 0; cb < D / 32; ++cb)
 #pragma unroll
             for (int x = 0; x < 16; ++x)
-                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(dk[kb][cb][x] * p.scale)), ko,
-                                                      lo, (cb * 32 + (x & 3) + 8 * (x >> 2)) * Nk * 2, 0);
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)(dk[cb][x] * p.scale)), ko, lo,
+                                                      (cb * 32 + (x & 3) + 8 * (x >> 2)) * Nk * 2, 0);
 #pragma unroll
         for (int cb = 0; cb < DV / 32; ++cb)
 #pragma unroll
             for (int x = 0; x < 16; ++x)
-                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)dv[kb][cb][x]), vo, lo,
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)dv[cb][x]), vo, lo,
                                                       (cb * 32 + (x & 3) + 8 * (x >> 2)) * Nk * 2, 0);
     }
 }
 
-#ifdef FA_BWD_STAMP4
-extern "C" int fa_debug_bwd_stamps(unsigned long long* out, int n) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamp), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
-}
-#endif
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
 thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
 thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD
@@ -1899,21 +1626,13 @@ thread_local int g_bwd_hoff = 3;            // bwd_fused: step offset between co
 thread_local int g_bwd_stall_us = kStallUs; // bwd_fused: no-progress bound of a poll (us)
 thread_local int g_bwd_nodirect = 0;         // bwd_fused (tests): every wrapped slice left to bwd_dq_fast's combine
 thread_local int g_bwd_xcd = -1;            // bwd_fused: one XCD per slab where eligible (-1 auto, 0 never)
-thread_local int g_bwd_waves = 8;           // bwd_fused at d = dv = 128: waves per workgroup
 
 template <class T, int D, int DV>
 static hipError_t launch_fast_dd(BwdParams p, hipStream_t s) {
     const bool fused = p.part != nullptr;
     if (fused) {   // single pass; dQ pass below only after a hand-off timeout
         p.total_wg = p.nkb * p.batch;
-        bool four = false;
-        if constexpr (D == 128 && DV == 128) {
-            if (g_bwd_waves == 4) {
-                hipLaunchKernelGGL((bwd_fused<T, D, DV, 4>), dim3((unsigned)p.total_wg), dim3(256), 0, s, p);
-                four = true;
-            }
-        }
-        if (!four) hipLaunchKernelGGL((bwd_fused<T, D, DV>), dim3((unsigned)p.total_wg), dim3(512), 0, s, p);
+        hipLaunchKernelGGL((bwd_fused<T, D, DV>), dim3((unsigned)p.total_wg), dim3(512), 0, s, p);
         const FusedFlags ff = fused_flags(p.batch, p.nqt, p.nkb);
         p.guard = p.err;
         p.sguard = p.flags + ff.serr;

@@ -149,7 +149,6 @@ extern thread_local int g_bwd_hoff;           // single pass: step offset betwee
 extern thread_local int g_bwd_stall_us;       // single pass: no-progress bound of a poll (us)
 extern thread_local int g_bwd_nodirect;       // single pass (tests): chain-B tails never add A's total themselves
 extern thread_local int g_bwd_xcd;            // single pass: one XCD per slab where eligible (-1 auto, 0 never)
-extern thread_local int g_bwd_waves;          // single pass at d = dv = 128: waves per workgroup (8 or 4)
 extern thread_local int g_win_force_composed; // windowed: forced path (composed / fused variants)
 extern thread_local int g_win_bwd_grid;       // windowed: strip backward workgroups (0: one per CU)
 extern thread_local int g_circ_force_generic; // circulant: forced kernel

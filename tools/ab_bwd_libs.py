@@ -35,16 +35,6 @@ for p in paths:
     if os.environ.get("AB_HOFF") is not None:
         libs[-1].fa_debug_set_bwd_hoff(int(os.environ["AB_HOFF"]))
 rounds = int(os.environ.get("AB_ROUNDS", 6))
-# AB_WAVES=8,4: the single pass's waves per workgroup, one entry per listed build (the
-# same build may be listed twice: the knob is set again before each of its calls)
-waves = [int(x) for x in os.environ["AB_WAVES"].split(",")] if os.environ.get("AB_WAVES") else None
-
-
-def use(i):
-    fa_hip._LIB = libs[i]
-    if waves:
-        assert libs[i].fa_debug_set_bwd_waves(waves[i]) != -2
-
 for (N, d, BH) in shapes:
     g = torch.Generator(device="cuda").manual_seed(1)
     mk = lambda: fa_hip.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"), torch.bfloat16)
@@ -58,7 +48,7 @@ for (N, d, BH) in shapes:
     fl = 4.0 * BH * N * N * d * 2.5
     outs = []
     for i, L in enumerate(libs):
-        use(i)
+        fa_hip._LIB = L
         outs.append([x.clone() for x in fa_hip.dense_fa_backward(Q, K, V, Oo, dO, l, m)])
         again = fa_hip.dense_fa_backward(Q, K, V, Oo, dO, l, m)
         torch.cuda.synchronize()
@@ -74,7 +64,7 @@ for (N, d, BH) in shapes:
     ts = [[] for _ in libs]
     for rnd in range(rounds):
         for i, L in enumerate(libs):
-            use(i)
+            fa_hip._LIB = L
             fa_hip.dense_fa_backward(Q, K, V, Oo, dO, l, m)
             e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -84,6 +74,5 @@ for (N, d, BH) in shapes:
             ts[i].append(e0.elapsed_time(e1) / 3 / 1e3)
     for i, p in enumerate(paths):
         t = float(np.median(ts[i]))
-        tag = os.path.basename(p) + (f" waves={waves[i]}" if waves else "")
-        print(f"N={N} d={d} BH={BH} {tag}: {t*1e3:.3f} ms  {fl/t/1e12:.1f} TFLOP/s "
+        print(f"N={N} d={d} BH={BH} {os.path.basename(p)}: {t*1e3:.3f} ms  {fl/t/1e12:.1f} TFLOP/s "
               f"(2.5x convention, {fl/t/1e12/PEAK*100:.1f}% peak)  best {fl/min(ts[i])/1e12:.1f}", flush=True)
