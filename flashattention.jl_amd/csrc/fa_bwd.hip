@@ -1105,6 +1105,22 @@ __device__ __forceinline__ void vm_wait() {
     __builtin_amdgcn_s_waitcnt(0x0F70 | N);
 }
 
+// Diagnostic phase stamps (tools/exp/bwd4_stamp.py; empty in the product build):
+// -DFA_BWD_STAMP4=w records s_memtime of workgroup w's first lane at phase points of
+// its first 128 steps (0 after B1, 8 end of phase A, 9 after B2, 10 end of the dQ phase).
+#ifdef FA_BWD_STAMP4
+__device__ unsigned long long g_bwd_stamp[128 * 16];
+#define BWD_STAMP(pt)                                                                          \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if (blockIdx.x == FA_BWD_STAMP4 && threadIdx.x == 0 && i < 128)                        \
+            g_bwd_stamp[i * 16 + (pt)] = __builtin_amdgcn_s_memtime();                         \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+    } while (0)
+#else
+#define BWD_STAMP(pt)
+#endif
+
 template <class T, int D, int DV>
 __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     typedef typename Frag8<T>::type F8;
@@ -1387,6 +1403,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             if (btail) s_direct[0] = !hc()->nodirect && ld_agent(hc()->fin + t) >= 1u ? 1u : 0u;
         }
         __syncthreads();
+        BWD_STAMP(0);
 
         // ---- S, dP, P, dS; dVᵀ, dKᵀ updates; dSᵀ into LDS ----
         const int pofs = lk.ch * pchain4 + (t * NTQ + wave) * 4096 + lq * 16;
@@ -1430,6 +1447,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 *(F8*)(dsimg + dsrow * 128 + (((4 * u + 2 * s2 + h) ^ swzds(dsrow)) * 16)) = dsf[s2];
         }
 
+        BWD_STAMP(8);
         // running sum of the members before this one (sc1 loads, after B1).  Loaded
         // whether or not this member is the chain's head (which adds nothing), and the
         // DMA and row constants below are unconditional too: a straight-line step
@@ -1472,6 +1490,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
             pa[3] = load16_sc1_asm<3072>(pdesc, pofa);
         }
         __syncthreads();   // B2: dSᵀ complete, the slice's images free, last step's sums stored
+        BWD_STAMP(9);
         // chain B's tail: whether A's total was there at the poll (lane 0's word, ordered
         // by B2).  Read and waited for here: the dQ phase below counts its own LDS reads
         // by hand (lgkm_wait), so no compiler-issued LDS read may land among them.
@@ -1588,6 +1607,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
                 }
             }
         }
+        BWD_STAMP(10);
         // publish kind: 0 none (dQ written), 1 chain count, 2 fin word (a wrapped chain's tail)
         const unsigned kind = (tail && !lk.wrap) || direct ? 0u : tail ? 2u : 1u;
         pub_prev = kind != 0u;
@@ -1618,6 +1638,11 @@ __global__ __launch_bounds__(512, 1) void bwd_fused(BwdParams p) {
     }
 }
 
+#ifdef FA_BWD_STAMP4
+extern "C" int fa_debug_bwd_stamps(unsigned long long* out, int n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamp), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 thread_local int g_bwd_force_generic = 0;   // benchmark knob
 thread_local int g_bwd_mode = 0;            // 0 auto, 1 split passes, 2 single pass where the shape allows
 thread_local int g_bwd_l2local = -1;        // bwd_fused: L2-local hand-off when a slab sits on one XCD

@@ -14,8 +14,9 @@ L = fa_hip.lib()
 buf = (ctypes.c_ulonglong * (128 * 16))()
 names = {0: "B1", 1: "SdP0", 2: "SdP1|V0", 3: "A0", 4: "SdP2|V1", 5: "A1", 6: "SdP3|V2", 7: "A2|V3", 8: "A3/phaseA",
          9: "B2", 10: "dQ"}
-for w in (8, 4):
-    L.fa_debug_set_bwd_waves(w)
+for w in ((8, 4) if hasattr(L, "fa_debug_set_bwd_waves") else (8,)):
+    if w != 8:
+        L.fa_debug_set_bwd_waves(w)
     for _ in range(3):
         fa_hip.dense_fa_backward(Q, K, V, O, dO, l, m)
     torch.cuda.synchronize()
