@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-O=gpurun_out/r6g; mkdir -p $O
+O=gpurun_out/r6h; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo tests failed; tail -30 $O/pytest_gpu.log; exit 1; }
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > $O/smoke.log 2>&1 || exit 2
 timeout -k 10 400 python bench.py > $O/bench_default.log 2>&1 || exit 3
