@@ -10,6 +10,6 @@ cp $C/fa_bwd.hip $B/fa_bwd.hip
 sed -i "s#\"fa_common.h\"#\"$C/fa_common.h\"#; s#\"fa_internal.h\"#\"$C/fa_internal.h\"#; s#\"../../include/fa_hip.h\"#\"/root/repo/include/fa_hip.h\"#" $B/fa_bwd.hip
 for e in "$@"; do python3 $e $B/fa_bwd.hip; done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-gpu-rdc -munsafe-fp-atomics $flags -x hip -c $B/fa_bwd.hip -o $B/fa_bwd.o
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out $C/build/api.cpp.o $C/build/fa_fwd.hip.o $C/build/fa_fwd_pers.hip.o $C/build/fa_fwd_p4.hip.o \
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out $C/build/api.cpp.o $C/build/fa_fwd.hip.o $C/build/fa_fwd_p4.hip.o \
     $B/fa_bwd.o $C/build/fa_windowed_fwd.o $C/build/fa_windowed_bwd.o $C/build/fa_circulant.hip.o $C/build/fa_softmax.hip.o $C/build/fa_f64.hip.o
 rm -rf $B

@@ -11,6 +11,8 @@ mk = lambda: fa_hip.jl_tensor(torch.randn((N, d, BH), generator=g, device="cuda"
 Q, K, V, dO = mk(), mk(), mk(), mk()
 O, l, m = fa_hip.dense_fa(Q, K, V)
 L = fa_hip.lib()
+if os.environ.get("FA_BWD_MODE"):   # timing-only ablations of a -DFA_BWD_ABL build (WRONG dQ)
+    assert L.fa_debug_set_bwd_mode(int(os.environ["FA_BWD_MODE"])) >= 0
 buf = (ctypes.c_ulonglong * (128 * 16))()
 names = {0: "B1", 1: "SdP0", 2: "SdP1|V0", 3: "A0", 4: "SdP2|V1", 5: "A1", 6: "SdP3|V2", 7: "A2|V3", 8: "A3/phaseA",
          9: "B2", 10: "dQ"}
