@@ -69,6 +69,23 @@ def test_exports_are_c_symbols_not_mangled():
         assert f in syms
 
 
+def test_product_library_carries_no_diagnostic_hooks():
+    # the phase-stamp reader and the timing-only ablation modes exist only in
+    # -DFA_BWD_STAMP4 / -DFA_BWD_ABL builds (tools/exp), never in the shipped library
+    import subprocess
+    import fa_hip
+    out = subprocess.run(["nm", "-D", "--defined-only", fa_hip.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert "fa_debug_bwd_stamps" not in syms
+    L = fa_hip.lib()
+    old = L.fa_debug_set_bwd_mode(0)
+    try:
+        assert L.fa_debug_set_bwd_mode(5) == -1, "timing-only ablation modes accepted by the product build"
+    finally:
+        L.fa_debug_set_bwd_mode(old)
+
+
 def _i(x):
     return ctypes.c_int64(x)
 
